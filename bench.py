@@ -1,0 +1,183 @@
+"""Benchmark of the MI355X OpenPose path: frames/s end-to-end (CNN + PAF grouping) at 368x368.
+
+python bench.py [--gpus N --steps K --warmup W --batch B]
+For N > 1 launch with torch.distributed.run (one process per GPU, RCCL gather of the per-frame
+result records to every rank).  A step = one batch of B frames per GPU through the whole path:
+uint8 BGR frame in HBM -> resize + normalise -> 92 convs -> upsample / Gaussian / NMS ->
+line integrals -> greedy assignment -> grouping -> poses copied to the host.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for every field.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "chainer_realtime_multi-person_pose_estimation_amd"
+METRIC = "frames/sec end-to-end (CNN+PAF grouping) at 368×368, 1/2/4/8 MI355X"
+FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_maps(batch):
+    """COCO-like last-stage maps (38 PAF + 19 heat at 46x46) of 6 people, from the reference's own
+    label generators (tests/golden/six_people.npz, made by tests/golden/make_golden.py)."""
+    d = np.load(os.path.join(REPO, "tests", "golden", "six_people.npz"))
+    m = np.concatenate([d["paf_low"], d["heat_low"]])[None]
+    return np.ascontiguousarray(np.repeat(m, batch, axis=0))
+
+
+def cpu_baseline(frames, maps, n_frames):
+    """The oracle (NumPy Chainer-CPU forward + C post-process restatement), timed per frame."""
+    from oracle import forward as F
+    from oracle import cvresize, postproc as P
+    import importlib
+    W = importlib.import_module(PKG + ".weights").random_weights(seed=0)
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([int(i.get("num_threads", 1)) for i in threadpool_info()] + [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    x = cvresize.preprocess(cvresize.resize_linear_u8(frames[0], 368, 368))
+    F.cocoposenet_forward(W, x)  # warm-up
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        f = frames[i % len(frames)]
+        x = cvresize.preprocess(cvresize.resize_linear_u8(f, 368, 368))
+        F.cocoposenet_forward(W, x)
+        P.postprocess(maps[i % len(maps), :38], maps[i % len(maps), 38:], f.shape[0], f.shape[1])
+    dt = time.perf_counter() - t0
+    return {"value": n_frames / dt, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": "%d frames: oracle im2col+sgemm forward (368x368, NumPy BLAS) + C post-process "
+                      "restatement on the same 6-person maps; %.1f s total" % (n_frames, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="frames per step per GPU")
+    ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
+                    help="post-process input: COCO-like 6-person maps (default) or the random-weight "
+                         "network's own last stage")
+    ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import importlib
+    L = importlib.import_module(PKG + "._lib")
+    Wm = importlib.import_module(PKG + ".weights")
+    Fr = importlib.import_module(PKG + ".frames")
+
+    B = args.batch
+    limits = L.OpLimits()
+    limits.max_batch = B
+    ctx = L.Context(local, None, limits)
+    ctx.set_weights(Wm.random_weights(seed=0))
+    rng = np.random.default_rng(1234 + rank)
+    frames = rng.integers(0, 256, (B, 368, 368, 3), dtype=np.uint8)
+    ctx.stage_frames(frames)
+    maps = synthetic_maps(B)
+    if args.maps == "synthetic":
+        ctx.stage_maps(maps)
+        ctx.use_staged_maps(True)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.all_reduce(torch.zeros(1, device="cuda"))
+            torch.cuda.synchronize()
+
+    persons = 0
+
+    def step(collect):
+        nonlocal persons
+        ctx.run_staged()
+        ctx.synchronize()
+        res = [ctx.fetch_result(i) for i in range(B)]
+        if collect:
+            persons += sum(r[2].n_persons for r in res)
+        if dist is not None:
+            import torch
+            recs = Fr.pack_records([(rank + world * i, r[2].status, r[2].n_peaks, r[0], r[1])
+                                    for i, r in enumerate(res)], 64)
+            Fr.gather_records(recs, 64, device=torch.device("cuda", local))
+
+    for _ in range(args.warmup):
+        step(False)
+    ctx.synchronize()
+    ctx.profile(not args.no_profile)
+    ctx.profile_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    ctx.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        pt = torch.tensor([float(persons)], device="cuda", dtype=torch.float64)
+        dist.all_reduce(pt)
+        persons = float(pt.item())
+
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+    ms7, n7, fl7, by7 = prof["conv7x7"]
+    roofline = None
+    if n7 > 0 and ms7 > 0:
+        achieved = fl7 / (ms7 * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": "conv_mfma_f32<7,2,2> (7x7 stage convs)",
+                    "achieved": round(achieved, 2), "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_MATRIX_PEAK_TFLOPS, 4), "traffic": None,
+                    "launch_ms": round(ms7 / n7, 4), "flops_per_launch": fl7 / n7,
+                    "algorithmic_bytes_per_launch": by7 / n7}
+    stage_ms = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: seeded uint8 368x368 BGR frames resident in HBM; random-init CocoPoseNet (He-normal); "
+                + ("post-process fed COCO-like 6-person network maps (reference label generators)"
+                   if args.maps == "synthetic" else "post-process fed the network's own last stage"),
+        "config": {"workload": "368x368 frames, full PoseDetector.__call__ path (resize+normalise, 92-conv "
+                               "CocoPoseNet fp32, PAF post-process), batch of %d frames per GPU per step" % B,
+                   "frames_per_step_per_gpu": B, "net_input": "368x368", "heatmap": "320x320",
+                   "maps": args.maps, "parallelism": "frame-parallel replicas x%d (RCCL gather of results)" % world},
+        "persons_per_s": round(persons / elapsed, 2),
+        "gflop_per_frame": round(L.forward_flops(368, 368) / 1e9, 2),
+        "stage_ms_per_step": stage_ms,
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(frames, maps, args.cpu_frames)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

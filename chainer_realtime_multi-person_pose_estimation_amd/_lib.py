@@ -1,0 +1,330 @@
+"""ctypes binding of libopenpose_hip.so (C ABI: include/openpose_hip.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot load, every entry point
+raises.  Status codes map to the exceptions the reference would raise (IndexError for the
+grouping overflow at pose_detector.py:197) or to RuntimeError/ValueError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libopenpose_hip.so")
+
+OP_OK, OP_ERR_INVALID, OP_ERR_HIP, OP_ERR_CAPACITY, OP_ERR_INDEX, OP_ERR_STATE = range(6)
+N_JOINTS, N_LIMBS, N_PAF, N_HEAT, N_LAYERS = 18, 19, 38, 19, 92
+
+# Every symbol include/openpose_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "op_last_error", "op_default_params", "op_default_limits", "op_layer_info", "op_create", "op_destroy",
+    "op_set_weights", "op_detect", "op_preprocess", "op_forward", "op_resize_images", "op_compute_peaks",
+    "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
+    "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
+    "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
+)
+
+
+class OpParams(ctypes.Structure):
+    _fields_ = [
+        ("inference_img_size", ctypes.c_int32), ("heatmap_size", ctypes.c_int32),
+        ("gaussian_sigma", ctypes.c_double), ("n_integ_points", ctypes.c_int32),
+        ("n_integ_points_thresh", ctypes.c_int32), ("heatmap_peak_thresh", ctypes.c_double),
+        ("inner_product_thresh", ctypes.c_double), ("limb_length_ratio", ctypes.c_double),
+        ("length_penalty_value", ctypes.c_double), ("n_subset_limbs_thresh", ctypes.c_int32),
+        ("subset_score_thresh", ctypes.c_double), ("limbs_point", (ctypes.c_int32 * 2) * N_LIMBS),
+        ("downscale", ctypes.c_int32),
+    ]
+
+
+class OpLimits(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "max_batch", "max_net_h", "max_net_w", "max_map_h", "max_map_w", "max_peaks_per_joint",
+        "max_frame_h", "max_frame_w")]
+
+
+class OpFrameResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "status", "n_peaks", "n_persons", "map_w", "map_h", "net_w", "net_h")]
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (fails loudly: there is no other implementation of this path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libopenpose_hip.so is not built (%s); run __graft_entry__.build() or "
+                           "make -C chainer_realtime_multi-person_pose_estimation_amd/csrc" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "op_last_error": ([], ctypes.c_char_p),
+        "op_default_params": ([P], ctypes.c_int),
+        "op_default_limits": ([P], ctypes.c_int),
+        "op_layer_info": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), P, P, P], ctypes.c_int),
+        "op_create": ([P, P, ctypes.c_int, P], ctypes.c_int),
+        "op_destroy": ([P], ctypes.c_int),
+        "op_set_weights": ([P, P, P], ctypes.c_int),
+        "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
+        "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
+        "op_forward": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
+        "op_resize_images": ([P, P, I32, I32, I32, I32, I32, P], ctypes.c_int),
+        "op_compute_peaks": ([P, P, I32, I32, I32, P, I64, P], ctypes.c_int),
+        "op_compute_connections": ([P, P, I32, I32, P, I64, D, P, I64, P], ctypes.c_int),
+        "op_grouping": ([P, P, P, P, I64, P, I64, P], ctypes.c_int),
+        "op_postprocess": ([P, P, P, I32, I32, I32, I32, P, P, I32, P], ctypes.c_int),
+        "op_stage_frames": ([P, P, I32, I32, I32], ctypes.c_int),
+        "op_stage_maps": ([P, P, I32, I32, I32], ctypes.c_int),
+        "op_use_staged_maps": ([P, I32], ctypes.c_int),
+        "op_run_staged": ([P], ctypes.c_int),
+        "op_run_staged_graph": ([P], ctypes.c_int),
+        "op_synchronize": ([P], ctypes.c_int),
+        "op_fetch_result": ([P, I32, P, P, I32, P], ctypes.c_int),
+        "op_last_timing": ([P, P, P, P], ctypes.c_int),
+        "op_forward_flops": ([I32, I32], D),
+        "op_profile_enable": ([P, I32], ctypes.c_int),
+        "op_profile_read": ([P, I32, P, P, P, P], ctypes.c_int),
+        "op_profile_reset": ([P], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def last_error():
+    return (lib().op_last_error() or b"").decode("utf-8", "replace")
+
+
+def check(rc, what=""):
+    if rc == OP_OK:
+        return
+    msg = "%s: %s" % (what, last_error()) if what else last_error()
+    if rc == OP_ERR_INDEX:
+        raise IndexError("list assignment index out of range")
+    if rc == OP_ERR_INVALID:
+        raise ValueError(msg)
+    raise RuntimeError("%s (status %d)" % (msg, rc))
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def default_params():
+    p = OpParams()
+    check(lib().op_default_params(ctypes.byref(p)))
+    return p
+
+
+def params_from_dict(d):
+    p = default_params()
+    for k in ("inference_img_size", "heatmap_size", "n_integ_points", "n_integ_points_thresh",
+              "n_subset_limbs_thresh", "downscale"):
+        if k in d:
+            setattr(p, k, int(d[k]))
+    for k in ("gaussian_sigma", "heatmap_peak_thresh", "inner_product_thresh", "limb_length_ratio",
+              "length_penalty_value", "subset_score_thresh"):
+        if k in d:
+            setattr(p, k, float(d[k]))
+    if "limbs_point" in d:
+        for i, (a, b) in enumerate(d["limbs_point"]):
+            p.limbs_point[i][0] = int(a)
+            p.limbs_point[i][1] = int(b)
+    return p
+
+
+def layer_table():
+    """[(name, ci, co, k)] in models/CocoPoseNet.py:26-129 order, from the library."""
+    out = []
+    name = ctypes.c_char_p()
+    ci, co, k = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    for i in range(N_LAYERS):
+        check(lib().op_layer_info(i, ctypes.byref(name), ctypes.byref(ci), ctypes.byref(co), ctypes.byref(k)))
+        out.append((name.value.decode(), ci.value, co.value, k.value))
+    return out
+
+
+def forward_flops(h, w):
+    return float(lib().op_forward_flops(int(h), int(w)))
+
+
+class Context(object):
+    """Owns one op_ctx (one device, one stream, packed weights in HBM)."""
+
+    def __init__(self, device=0, params=None, limits=None):
+        L = lib()
+        self._p = params if params is not None else default_params()
+        self._l = limits if limits is not None else OpLimits()
+        h = ctypes.c_void_p()
+        check(L.op_create(ctypes.byref(self._p), ctypes.byref(self._l), int(device), ctypes.byref(h)), "op_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().op_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_weights(self, weights):
+        """weights: {layer name: (W (Co,Ci,k,k) f32, b (Co,) f32)}."""
+        table = layer_table()
+        keep = []
+        Wp = (ctypes.c_void_p * N_LAYERS)()
+        bp = (ctypes.c_void_p * N_LAYERS)()
+        for i, (name, ci, co, k) in enumerate(table):
+            if name not in weights:
+                raise KeyError("missing weights for layer %s" % name)
+            W, b = weights[name]
+            W = np.ascontiguousarray(W, dtype=np.float32)
+            b = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+            if W.shape != (co, ci, k, k) or b.shape != (co,):
+                raise ValueError("layer %s: expected W%s b(%d,), got %s %s" % (name, (co, ci, k, k), co, W.shape, b.shape))
+            keep += [W, b]
+            Wp[i] = W.ctypes.data
+            bp[i] = b.ctypes.data
+        check(lib().op_set_weights(self.h, Wp, bp), "op_set_weights")
+
+    # ---- results ----
+    def _result_arrays(self, cap):
+        return np.empty((cap, N_JOINTS, 3), np.float64), np.empty(cap, np.float64), OpFrameResult()
+
+    def detect(self, img, cap=2048):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        if img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        poses, scores, res = self._result_arrays(cap)
+        check(lib().op_detect(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], ptr(poses), ptr(scores),
+                              cap, ctypes.byref(res)), "op_detect")
+        return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    def preprocess(self, img, out_w, out_h):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        x = np.empty((1, 3, out_h, out_w), np.float32)
+        check(lib().op_preprocess(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], out_w, out_h, ptr(x)),
+              "op_preprocess")
+        return x
+
+    def forward(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n, c, h, w = x.shape
+        if c != 3:
+            raise ValueError("expected (n, 3, h, w)")
+        paf = np.empty((n, N_PAF, h // 8, w // 8), np.float32)
+        heat = np.empty((n, N_HEAT, h // 8, w // 8), np.float32)
+        check(lib().op_forward(self.h, ptr(x), n, h, w, ptr(paf), ptr(heat)), "op_forward")
+        return paf, heat
+
+    def resize_images(self, x, oh, ow):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        c, h, w = x.shape
+        y = np.empty((c, oh, ow), np.float32)
+        check(lib().op_resize_images(self.h, ptr(x), c, h, w, oh, ow, ptr(y)), "op_resize_images")
+        return y
+
+    def compute_peaks(self, heatmaps):
+        heatmaps = np.ascontiguousarray(heatmaps, dtype=np.float32)
+        c, h, w = heatmaps.shape
+        cap = max(1, N_JOINTS * 2048)
+        out = np.empty((cap, 5), np.float64)
+        n = ctypes.c_int64()
+        check(lib().op_compute_peaks(self.h, ptr(heatmaps), c, h, w, ptr(out), cap, ctypes.byref(n)),
+              "op_compute_peaks")
+        return out[:n.value].copy()
+
+    def compute_connections(self, pafs, peaks, img_len):
+        pafs = np.ascontiguousarray(pafs, dtype=np.float32)
+        peaks = np.ascontiguousarray(np.asarray(peaks, np.float64).reshape(-1, 5))
+        _, h, w = pafs.shape
+        cap = max(1, N_LIMBS * 2048)
+        conn = np.empty((cap, 3), np.float64)
+        off = np.zeros(N_LIMBS + 1, np.int64)
+        check(lib().op_compute_connections(self.h, ptr(pafs), h, w, ptr(peaks), len(peaks), float(img_len), ptr(conn),
+                                           cap, ptr(off)), "op_compute_connections")
+        return [conn[off[l]:off[l + 1]].copy() for l in range(N_LIMBS)]
+
+    def grouping(self, connections, peaks):
+        peaks = np.ascontiguousarray(np.asarray(peaks, np.float64).reshape(-1, 5))
+        rows = [np.asarray(c, np.float64).reshape(-1, 3) for c in connections]
+        conn = np.ascontiguousarray(np.concatenate(rows) if rows else np.zeros((0, 3)))
+        off = np.zeros(N_LIMBS + 1, np.int64)
+        off[1:] = np.cumsum([len(r) for r in rows])
+        cap = 2048
+        subsets = np.empty((cap, 20), np.float64)
+        n = ctypes.c_int64()
+        check(lib().op_grouping(self.h, ptr(conn if len(conn) else np.zeros((1, 3))), ptr(off), ptr(peaks), len(peaks),
+                                ptr(subsets), cap, ctypes.byref(n)), "op_grouping")
+        return subsets[:n.value].copy()
+
+    def postprocess(self, paf_low, heat_low, orig_h, orig_w, cap=2048):
+        paf_low = np.ascontiguousarray(paf_low, dtype=np.float32)
+        heat_low = np.ascontiguousarray(heat_low, dtype=np.float32)
+        _, h, w = paf_low.shape
+        poses, scores, res = self._result_arrays(cap)
+        check(lib().op_postprocess(self.h, ptr(paf_low), ptr(heat_low), h, w, int(orig_h), int(orig_w), ptr(poses),
+                                   ptr(scores), cap, ctypes.byref(res)), "op_postprocess")
+        return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    # ---- staged batched path ----
+    def stage_frames(self, frames):
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        n, h, w, c = frames.shape
+        check(lib().op_stage_frames(self.h, ptr(frames), n, h, w), "op_stage_frames")
+
+    def stage_maps(self, maps):
+        maps = np.ascontiguousarray(maps, dtype=np.float32)
+        n, c, h, w = maps.shape
+        if c != N_PAF + N_HEAT:
+            raise ValueError("maps must be (n, 57, h, w): 38 PAF then 19 heatmap channels")
+        check(lib().op_stage_maps(self.h, ptr(maps), n, h, w), "op_stage_maps")
+
+    def use_staged_maps(self, enable):
+        check(lib().op_use_staged_maps(self.h, 1 if enable else 0))
+
+    def run_staged(self, graph=False):
+        check((lib().op_run_staged_graph if graph else lib().op_run_staged)(self.h), "op_run_staged")
+
+    def synchronize(self):
+        check(lib().op_synchronize(self.h), "op_synchronize")
+
+    def fetch_result(self, frame, cap=2048):
+        poses, scores, res = self._result_arrays(cap)
+        check(lib().op_fetch_result(self.h, int(frame), ptr(poses), ptr(scores), cap, ctypes.byref(res)),
+              "op_fetch_result")
+        return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    def last_timing(self):
+        a, b, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(lib().op_last_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(t)), "op_last_timing")
+        return a.value, b.value, t.value
+
+    # ---- per-kernel-class event timing ----
+    PROFILE_CLASSES = ("conv7x7", "conv3x3", "conv1x1", "postprocess")
+
+    def profile(self, enable=True):
+        check(lib().op_profile_enable(self.h, 1 if enable else 0), "op_profile_enable")
+
+    def profile_reset(self):
+        check(lib().op_profile_reset(self.h), "op_profile_reset")
+
+    def profile_read(self):
+        """{class: (ms, launches, algorithmic flops, algorithmic bytes)} since the last reset."""
+        out = {}
+        for i, name in enumerate(self.PROFILE_CLASSES):
+            ms, n, fl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+            check(lib().op_profile_read(self.h, i, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
+                                        ctypes.byref(by)), "op_profile_read")
+            out[name] = (ms.value, n.value, fl.value, by.value)
+        return out

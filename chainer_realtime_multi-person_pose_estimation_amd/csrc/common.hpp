@@ -1,0 +1,128 @@
+// Shared helpers for the gfx950 kernels and the runtime.  Compiled with -ffp-contract=off:
+// every fused multiply-add in the numeric-parity kernels is written explicitly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "openpose_hip.h"
+
+namespace op {
+
+// Thread-local last error text for op_last_error().
+void set_error(const std::string& msg);
+
+#define OP_HIP_CHECK(expr)                                                                   \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      ::op::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                    \
+      return OP_ERR_HIP;                                                                     \
+    }                                                                                        \
+  } while (0)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// Physical channel layout of the 185-channel stage input (F.concat((paf, heat, feature)),
+// CocoPoseNet.py:168): feature first so every slice start is 16-B aligned for the stores.
+constexpr int kCatStride = 192;
+constexpr int kCatFeat = 0;    // 128 channels
+constexpr int kCatHeat = 128;  // 19 channels (+1 zero pad)
+constexpr int kCatPaf = 148;   // 38 channels (+2 zero pad)
+constexpr int kStagePad = 3;   // halo of the 7x7 stage convs
+
+// ---- launch helpers implemented in the .hip files ----
+struct ConvGroup {
+  const float* in;    // padded NHWC input, already offset by the group's first input channel
+  float* out;         // padded NHWC output, already offset by the group's first output channel
+  const float* w;     // packed weights [c8][tap][cop][8]
+  const float* bias;  // [cop]
+  int32_t cop;        // padded output channels (multiple of the co tile)
+  int32_t cout_store; // channels actually written (multiple of 4)
+};
+
+struct ConvShape {
+  int32_t n, h, w;       // batch and spatial size (stride 1, same padding)
+  int32_t pin, cs_in;    // input buffer halo and channel stride
+  int32_t pout, cs_out;  // output buffer halo and channel stride
+  int32_t c8;            // input channels / 8
+  int32_t ks;            // 1, 3, 7
+  int32_t relu;
+  int32_t groups;        // 1 or 2
+};
+
+int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st);
+int launch_maxpool2(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
+                    int32_t c, hipStream_t st);
+int launch_nchw_to_nhwc8(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);
+int launch_extract_maps(const float* cat, int32_t n, int32_t h, int32_t w, float* paf, float* heat, hipStream_t st);
+int launch_preprocess(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t n, int32_t sh,
+                      int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st);
+int launch_preprocess_planar(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t dh,
+                             int32_t dw, float* out_nchw, hipStream_t st);
+
+// Post-process device state for a batch of frames.
+struct PostBuffers {
+  int32_t maxp;        // peaks per joint cap
+  int64_t maxc;        // candidates per limb cap (= maxp*maxp)
+  int32_t maxs;        // subsets per frame cap (= 19*maxp)
+  float* up;           // [B][18][Hm][Wm] upsampled heat
+  float* tmp;          // [B][18][Hm][Wm] vertical pass
+  float* hm;           // [B][18][Hm][Wm] filtered
+  int32_t* peak_xy;    // [B][18][maxp]  x | y << 16
+  float* peak_score;   // [B][18][maxp]
+  int32_t* peak_cnt;   // [B][18]
+  double* cand_score;  // [B][19][maxc]
+  int32_t* cand_idx;   // [B][19][maxc]
+  int32_t* cand_cnt;   // [B][19]
+  int32_t* conn_ab;    // [B][19][maxp][2] global peak ids
+  double* conn_score;  // [B][19][maxp]
+  int32_t* conn_cnt;   // [B][19]
+  int32_t* sub_ids;    // [B][maxs][18]
+  double* sub_sc;      // [B][maxs][2]  score, count
+  double* res_poses;   // [B][maxs][18][3]
+  double* res_scores;  // [B][maxs]
+  double* res_subsets; // [B][maxs][20] kept subset rows (grouping_key_points output)
+  int32_t* res_hdr;    // [B][4]: status, n_peaks, n_persons, reserved
+  double* gauss_w;     // [21] device copy of the Gaussian taps
+};
+
+struct PostShape {
+  int32_t n;             // frames
+  int32_t lh, lw;        // network map size (low res)
+  int32_t mh, mw;        // post-process map size
+  int32_t radius;        // Gaussian radius (10)
+  double img_len;        // distance-prior length (map_w, pose_detector.py:511)
+  double sx, sy;         // output rescale (orig_w / map_w, orig_h / map_h; 1 in precise mode)
+  float peak_thresh;
+  int32_t n_integ;       // 10
+  int32_t n_integ_thresh;// 8
+  double inner_thresh, len_ratio, len_penalty;
+  int32_t subset_min;    // 3
+  double subset_score;   // 0.2
+  int32_t limbs[OP_N_LIMBS][2];
+};
+
+// Low-res network maps as the post-process reads them: the stage-input (concat) NHWC buffer layout,
+// element (frame f, map channel c, y, x) at base + f*fstride + ((y+pad)*(lw+2*pad) + x+pad)*cs + c.
+struct MapSource {
+  const float* base;
+  int64_t fstride;
+  int32_t pad;
+  int32_t cs;
+  int32_t paf_off;   // channel of PAF 0
+  int32_t heat_off;  // channel of heatmap 0
+};
+
+int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, hipStream_t st);
+// Sub-steps on already-upsampled inputs (stage-level ABI)
+int launch_peaks_from_full(const float* heat_full, int32_t n_joint, int32_t mh, int32_t mw, const PostShape& s,
+                           PostBuffers& b, hipStream_t st);
+int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const PostShape& s, PostBuffers& b,
+                            hipStream_t st);
+int launch_grouping(const PostShape& s, PostBuffers& b, hipStream_t st);
+int launch_resize_images(const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y,
+                         hipStream_t st);
+
+}  // namespace op

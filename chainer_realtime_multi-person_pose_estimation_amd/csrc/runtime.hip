@@ -1,0 +1,1337 @@
+// Runtime + C ABI of the MI355X OpenPose path (include/openpose_hip.h).
+//
+// One context = one device, one stream, weights packed once in HBM, an activation arena carved
+// per (batch, net size) geometry, and the post-process buffers.  The forward plan is the layer
+// sequence of models/CocoPoseNet.py:132-262 with the two refinement branches fused:
+//   * Mconv1_stageN_L1/L2 and conv5_1_CPM_L1/L2 share their input -> one conv with Co = 256;
+//   * the later branch layers run as one 2-group launch (grid.z = branch);
+//   * F.concat((paf, heat, feature)) is a single 192-channel buffer whose slices the producing
+//     convs write directly (no concat copy).
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace op {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+struct LayerDef {
+  const char* name;
+  int ci, co, k;
+};
+
+// models/CocoPoseNet.py:26-129 declaration order.
+static std::vector<LayerDef> make_layers() {
+  std::vector<LayerDef> v;
+  static const char* bb[] = {"conv1_1", "conv1_2", "conv2_1", "conv2_2", "conv3_1", "conv3_2",
+                             "conv3_3", "conv3_4", "conv4_1", "conv4_2", "conv4_3_CPM", "conv4_4_CPM"};
+  static const int bci[] = {3, 64, 64, 128, 128, 256, 256, 256, 256, 512, 512, 256};
+  static const int bco[] = {64, 64, 128, 128, 256, 256, 256, 256, 512, 512, 256, 128};
+  for (int i = 0; i < 12; ++i) v.push_back({bb[i], bci[i], bco[i], 3});
+  static std::vector<std::string> names;  // storage for generated names
+  names.reserve(200);
+  auto add = [&](const std::string& n, int ci, int co, int k) {
+    names.push_back(n);
+    v.push_back({names.back().c_str(), ci, co, k});
+  };
+  const char* br[2] = {"L1", "L2"};
+  const int out[2] = {38, 19};
+  for (int b = 0; b < 2; ++b) {
+    for (int i = 1; i <= 3; ++i) add("conv5_" + std::to_string(i) + "_CPM_" + br[b], 128, 128, 3);
+    add(std::string("conv5_4_CPM_") + br[b], 128, 512, 1);
+    add(std::string("conv5_5_CPM_") + br[b], 512, out[b], 1);
+  }
+  for (int s = 2; s <= 6; ++s)
+    for (int b = 0; b < 2; ++b) {
+      const std::string sfx = "_stage" + std::to_string(s) + "_" + br[b];
+      add("Mconv1" + sfx, 185, 128, 7);
+      for (int i = 2; i <= 5; ++i) add("Mconv" + std::to_string(i) + sfx, 128, 128, 7);
+      add("Mconv6" + sfx, 128, 128, 1);
+      add("Mconv7" + sfx, 128, out[b], 1);
+    }
+  return v;
+}
+
+static const std::vector<LayerDef>& layers() {
+  static std::vector<LayerDef> L = make_layers();
+  return L;
+}
+
+static int layer_index(const std::string& n) {
+  const auto& L = layers();
+  for (size_t i = 0; i < L.size(); ++i)
+    if (n == L[i].name) return (int)i;
+  return -1;
+}
+
+// ---- packed weights ----
+struct PackedConv {
+  float* w = nullptr;
+  float* b = nullptr;
+  int cop = 0, cin_phys = 0, ks = 0;
+  int cin_log = 0, co_log = 0;  // logical (reference) channel counts, for algorithmic FLOPs
+};
+
+struct ProfPair {
+  int cls;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+
+// Logical input channel of physical channel p in the stage-input buffer (-1 = zero pad).
+// Logical order is F.concat((paf 38, heat 19, feature 128)) (CocoPoseNet.py:168).
+static int cat_logical(int p) {
+  if (p >= kCatFeat && p < kCatFeat + 128) return 57 + (p - kCatFeat);
+  if (p >= kCatHeat && p < kCatHeat + 19) return 38 + (p - kCatHeat);
+  if (p >= kCatPaf && p < kCatPaf + 38) return p - kCatPaf;
+  return -1;
+}
+
+// Pack Chainer W (Co, Ci, k, k) into [c8][tap][cop][8] at output-channel offset co_off.
+static void pack_into(std::vector<float>& dst, std::vector<float>& bias, int cop, int cin_phys, int k, const float* W,
+                      const float* b, int Co, int Ci, int co_off, bool cat_input) {
+  const int c8 = cin_phys / 8, taps = k * k;
+  for (int co = 0; co < Co; ++co) {
+    bias[co_off + co] = b[co];
+    for (int p = 0; p < cin_phys; ++p) {
+      const int ci = cat_input ? cat_logical(p) : (p < Ci ? p : -1);
+      if (ci < 0) continue;
+      for (int t = 0; t < taps; ++t) {
+        const int ky = t / k, kx = t % k;
+        const float v = W[(((size_t)co * Ci + ci) * k + ky) * k + kx];
+        const size_t idx = ((((size_t)(p / 8) * taps + t) * cop) + (co_off + co)) * 8 + (p % 8);
+        dst[idx] = v;
+      }
+    }
+  }
+  (void)c8;
+}
+
+static int upload(PackedConv& pc, const std::vector<float>& w, const std::vector<float>& b) {
+  OP_HIP_CHECK(hipMalloc(&pc.w, w.size() * sizeof(float)));
+  OP_HIP_CHECK(hipMalloc(&pc.b, b.size() * sizeof(float)));
+  OP_HIP_CHECK(hipMemcpy(pc.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+  OP_HIP_CHECK(hipMemcpy(pc.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+  return OP_OK;
+}
+
+static int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// ---- activation buffers ----
+struct Act {
+  float* p = nullptr;
+  int pad = 0, cs = 0, h = 0, w = 0;
+  size_t frame_floats() const { return (size_t)(h + 2 * pad) * (w + 2 * pad) * cs; }
+};
+
+enum BufId {
+  B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
+  B_S1, B_COUNT
+};
+
+}  // namespace op
+
+using namespace op;
+
+struct op_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  op_params prm;
+  op_limits lim;
+  bool have_weights = false;
+  // packed convolutions (see build_weights)
+  PackedConv bb[12];           // backbone conv1_1 .. conv4_4_CPM
+  PackedConv s1_first;         // conv5_1 L1|L2 fused (Co 256)
+  PackedConv s1_g[2][3];       // [branch][conv5_2, conv5_3, conv5_4]
+  PackedConv s1_last[2];       // conv5_5 L1 / L2
+  PackedConv st_first[5];      // Mconv1 stage s, fused (Co 256, 192 phys in)
+  PackedConv st_g[5][2][5];    // [stage][branch][Mconv2..Mconv6]
+  PackedConv st_last[5][2];    // Mconv7
+  // activation arena
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  int gn = 0, gh = 0, gw = 0;  // current geometry (batch, net h, net w)
+  Act buf[B_COUNT];
+  // post-process
+  PostBuffers pb{};
+  void* post_arena = nullptr;
+  size_t post_bytes = 0;
+  int pn = 0, pmh = 0, pmw = 0;  // post geometry
+  std::vector<double> gauss_host;
+  int gauss_r = 0;
+  // staging
+  uint8_t* d_frames = nullptr;
+  size_t frames_bytes = 0;
+  int st_n = 0, st_h = 0, st_w = 0;
+  float* d_maps = nullptr;
+  size_t maps_bytes = 0;
+  int sm_n = 0, sm_h = 0, sm_w = 0;
+  bool use_maps = false;
+  float* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  // timing
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool timed = false;
+  // per-class launch profiling
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<op::ProfPair> pending;
+  double prof_ms[4] = {0, 0, 0, 0}, prof_flops[4] = {0, 0, 0, 0}, prof_bytes[4] = {0, 0, 0, 0};
+  int64_t prof_n[4] = {0, 0, 0, 0};
+  // graph
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  uintptr_t g_key[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+namespace op {
+
+static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out) {
+  // (pad, channel stride, scale divisor) per buffer
+  struct D {
+    int pad, cs, div;
+  };
+  const D d[B_COUNT] = {{1, 8, 1},   {1, 64, 1},  {0, 64, 1},  {1, 64, 2},  {1, 128, 2}, {0, 128, 2},
+                        {1, 128, 4}, {1, 256, 4}, {1, 256, 4}, {0, 256, 4}, {1, 256, 8}, {1, 512, 8},
+                        {1, 512, 8}, {1, 256, 8}, {kStagePad, kCatStride, 8}, {kStagePad, 256, 8},
+                        {kStagePad, 256, 8}, {0, 1024, 8}};
+  size_t total = 0;
+  for (int i = 0; i < B_COUNT; ++i) {
+    Act a;
+    a.pad = d[i].pad;
+    a.cs = d[i].cs;
+    a.h = h / d[i].div;
+    a.w = w / d[i].div;
+    const size_t fl = a.frame_floats() * (size_t)n;
+    if (out) {
+      out[i] = a;
+      out[i].p = nullptr;
+    }
+    total += (fl + 63) / 64 * 64;  // 256-B alignment
+  }
+  (void)c;
+  return total;
+}
+
+static int ensure_geometry(op_ctx* c, int n, int h, int w) {
+  if (h % 8 || w % 8 || h < 16 || w < 16 || n < 1) {
+    set_error("network input must be >= 16 and a multiple of 8");
+    return OP_ERR_INVALID;
+  }
+  if (c->gn == n && c->gh == h && c->gw == w) return OP_OK;
+  Act a[B_COUNT];
+  const size_t need = geom_floats(c, n, h, w, a) * sizeof(float);
+  if (need > c->arena_bytes) {
+    if (c->arena) OP_HIP_CHECK(hipFree(c->arena));
+    c->arena = nullptr;
+    OP_HIP_CHECK(hipMalloc(&c->arena, need));
+    c->arena_bytes = need;
+  }
+  float* p = (float*)c->arena;
+  for (int i = 0; i < B_COUNT; ++i) {
+    a[i].p = p;
+    const size_t fl = a[i].frame_floats() * (size_t)n;
+    p += (fl + 63) / 64 * 64;
+    c->buf[i] = a[i];
+  }
+  // zero halos (and everything else) once per geometry; kernels only ever write interiors
+  OP_HIP_CHECK(hipMemsetAsync(c->arena, 0, need, c->stream));
+  c->gn = n;
+  c->gh = h;
+  c->gw = w;
+  return OP_OK;
+}
+
+static int ensure_post(op_ctx* c, int n, int mh, int mw) {
+  if (c->pn >= n && c->pmh * c->pmw >= mh * mw && c->pb.up) return OP_OK;
+  const int nn = std::max(n, c->pn), area = std::max(mh * mw, c->pmh * c->pmw);
+  PostBuffers b{};
+  b.maxp = c->lim.max_peaks_per_joint;
+  b.maxc = (int64_t)b.maxp * b.maxp;
+  b.maxs = OP_N_LIMBS * b.maxp;
+  if (b.maxs > 2048) b.maxs = 2048;
+  struct Part {
+    void** p;
+    size_t bytes;
+  };
+  const size_t plane = (size_t)nn * OP_N_JOINTS * area * sizeof(float);
+  std::vector<Part> parts = {
+      {(void**)&b.up, plane},
+      {(void**)&b.tmp, plane},
+      {(void**)&b.hm, plane},
+      {(void**)&b.peak_xy, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
+      {(void**)&b.peak_score, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
+      {(void**)&b.peak_cnt, (size_t)nn * OP_N_JOINTS * 4},
+      {(void**)&b.cand_score, (size_t)nn * OP_N_LIMBS * b.maxc * 8},
+      {(void**)&b.cand_idx, (size_t)nn * OP_N_LIMBS * b.maxc * 4},
+      {(void**)&b.cand_cnt, (size_t)nn * OP_N_LIMBS * 4},
+      {(void**)&b.conn_ab, (size_t)nn * OP_N_LIMBS * b.maxp * 8},
+      {(void**)&b.conn_score, (size_t)nn * OP_N_LIMBS * b.maxp * 8},
+      {(void**)&b.conn_cnt, (size_t)nn * OP_N_LIMBS * 4},
+      {(void**)&b.sub_ids, 16},
+      {(void**)&b.sub_sc, 16},
+      {(void**)&b.res_poses, (size_t)nn * b.maxs * OP_N_JOINTS * 3 * 8},
+      {(void**)&b.res_scores, (size_t)nn * b.maxs * 8},
+      {(void**)&b.res_subsets, (size_t)nn * b.maxs * 20 * 8},
+      {(void**)&b.res_hdr, (size_t)nn * 4 * 4},
+      {(void**)&b.gauss_w, 64 * 8},
+  };
+  size_t total = 0;
+  for (auto& q : parts) total += (q.bytes + 255) / 256 * 256;
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->post_arena) OP_HIP_CHECK(hipFree(c->post_arena));
+  c->post_arena = nullptr;
+  OP_HIP_CHECK(hipMalloc(&c->post_arena, total));
+  c->post_bytes = total;
+  char* p = (char*)c->post_arena;
+  for (auto& q : parts) {
+    *q.p = p;
+    p += (q.bytes + 255) / 256 * 256;
+  }
+  OP_HIP_CHECK(hipMemset(c->post_arena, 0, total));
+  OP_HIP_CHECK(hipMemcpy(b.gauss_w, c->gauss_host.data(), c->gauss_host.size() * 8, hipMemcpyHostToDevice));
+  c->pb = b;
+  c->pn = nn;
+  c->pmh = mh;
+  c->pmw = area / mh;
+  if (c->gexec) {
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  return OP_OK;
+}
+
+static int ensure_scratch(op_ctx* c, size_t bytes) {
+  if (bytes <= c->scratch_bytes) return OP_OK;
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->d_scratch) OP_HIP_CHECK(hipFree(c->d_scratch));
+  c->d_scratch = nullptr;
+  OP_HIP_CHECK(hipMalloc(&c->d_scratch, bytes));
+  c->scratch_bytes = bytes;
+  return OP_OK;
+}
+
+// ---- forward plan ----
+static ConvGroup grp(const Act& in, int cin_off, const Act& out, int cout_off, const PackedConv& pc, int cout_store) {
+  ConvGroup g;
+  g.in = in.p + cin_off;
+  g.out = out.p + cout_off;
+  g.w = pc.w;
+  g.bias = pc.b;
+  g.cop = pc.cop;
+  g.cout_store = cout_store;
+  return g;
+}
+
+static ConvShape shp(int n, const Act& in, const Act& out, int c8, int ks, bool relu, int groups) {
+  ConvShape s;
+  s.n = n;
+  s.h = out.h;
+  s.w = out.w;
+  s.pin = in.pad;
+  s.cs_in = in.cs;
+  s.pout = out.pad;
+  s.cs_out = out.cs;
+  s.c8 = c8;
+  s.ks = ks;
+  s.relu = relu ? 1 : 0;
+  s.groups = groups;
+  return s;
+}
+
+static hipEvent_t pool_event(op_ctx* c) {
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[c->ev_used++];
+}
+
+// Record an event pair around `fn`'s launches when profiling is on.
+template <class Fn>
+static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
+  if (!c->prof) return fn();
+  hipEvent_t a = pool_event(c), b = pool_event(c);
+  if (!a || !b) return fn();
+  OP_HIP_CHECK(hipEventRecord(a, c->stream));
+  const int rc = fn();
+  OP_HIP_CHECK(hipEventRecord(b, c->stream));
+  c->pending.push_back(ProfPair{cls, a, b, flops, bytes});
+  return rc;
+}
+
+static int conv_class(int ks) { return ks == 7 ? 0 : (ks == 3 ? 1 : 2); }
+
+// algorithmic work of one conv group: 2*Ci*Co*k*k*N*H*W FLOPs; bytes = input + output + weights (fp32)
+static void conv_work(const op_ctx* c, const Act& out, const PackedConv& pc, double* flops, double* bytes) {
+  const double px = (double)c->gn * out.h * out.w;
+  *flops += 2.0 * pc.cin_log * pc.co_log * pc.ks * pc.ks * px;
+  *bytes += 4.0 * (px * pc.cin_log + px * pc.co_log + (double)pc.cin_log * pc.co_log * pc.ks * pc.ks + pc.co_log);
+}
+
+static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout_off, const PackedConv& pc, int store,
+                 bool relu) {
+  ConvGroup g[2];
+  g[0] = grp(in, cin_off, out, cout_off, pc, store);
+  g[1] = g[0];
+  double fl = 0, by = 0;
+  conv_work(c, out, pc, &fl, &by);
+  return profiled(c, conv_class(pc.ks), fl, by,
+                  [&] { return launch_conv(shp(c->gn, in, out, pc.cin_phys / 8, pc.ks, relu, 1), g, c->stream); });
+}
+
+static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1, const PackedConv& p0,
+                 const PackedConv& p1, int st0, int st1, bool relu) {
+  ConvGroup g[2];
+  g[0] = grp(in, ci0, out, co0, p0, st0);
+  g[1] = grp(in, ci1, out, co1, p1, st1);
+  double fl = 0, by = 0;
+  conv_work(c, out, p0, &fl, &by);
+  conv_work(c, out, p1, &fl, &by);
+  return profiled(c, conv_class(p0.ks), fl, by,
+                  [&] { return launch_conv(shp(c->gn, in, out, p0.cin_phys / 8, p0.ks, relu, 2), g, c->stream); });
+}
+
+#define RC(x)            \
+  do {                   \
+    int _r = (x);        \
+    if (_r) return _r;   \
+  } while (0)
+
+static int run_forward(op_ctx* c) {
+  Act* B = c->buf;
+  RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
+  RC(conv1(c, B[B_C11], 0, B[B_C12], 0, c->bb[1], 64, true));
+  RC(launch_maxpool2(B[B_C12].p, 0, B[B_P1].p, 1, c->gn, B[B_C12].h, B[B_C12].w, 64, c->stream));
+  RC(conv1(c, B[B_P1], 0, B[B_C21], 0, c->bb[2], 128, true));
+  RC(conv1(c, B[B_C21], 0, B[B_C22], 0, c->bb[3], 128, true));
+  RC(launch_maxpool2(B[B_C22].p, 0, B[B_P2].p, 1, c->gn, B[B_C22].h, B[B_C22].w, 128, c->stream));
+  RC(conv1(c, B[B_P2], 0, B[B_C3A], 0, c->bb[4], 256, true));
+  RC(conv1(c, B[B_C3A], 0, B[B_C3B], 0, c->bb[5], 256, true));
+  RC(conv1(c, B[B_C3B], 0, B[B_C3A], 0, c->bb[6], 256, true));
+  RC(conv1(c, B[B_C3A], 0, B[B_C34], 0, c->bb[7], 256, true));
+  RC(launch_maxpool2(B[B_C34].p, 0, B[B_P3].p, 1, c->gn, B[B_C34].h, B[B_C34].w, 256, c->stream));
+  RC(conv1(c, B[B_P3], 0, B[B_C41], 0, c->bb[8], 512, true));
+  RC(conv1(c, B[B_C41], 0, B[B_C42], 0, c->bb[9], 512, true));
+  RC(conv1(c, B[B_C42], 0, B[B_C43], 0, c->bb[10], 256, true));
+  RC(conv1(c, B[B_C43], 0, B[B_CAT], kCatFeat, c->bb[11], 128, true));
+  // stage 1 (CocoPoseNet.py:153-165)
+  const Act& cat = B[B_CAT];
+  Act s1 = B[B_S1];
+  RC(conv1(c, cat, kCatFeat, B[B_BRA], 0, c->s1_first, 256, true));
+  RC(conv2(c, B[B_BRA], 0, 128, B[B_BRB], 0, 128, c->s1_g[0][0], c->s1_g[1][0], 128, 128, true));
+  RC(conv2(c, B[B_BRB], 0, 128, B[B_BRA], 0, 128, c->s1_g[0][1], c->s1_g[1][1], 128, 128, true));
+  RC(conv2(c, B[B_BRA], 0, 128, s1, 0, 512, c->s1_g[0][2], c->s1_g[1][2], 512, 512, true));
+  RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false));
+  // stages 2-6 (CocoPoseNet.py:167-260)
+  Act s6 = B[B_S1];
+  s6.cs = 256;  // Mconv6 output reuses the stage-1 1x1 buffer (no halo) with a 256-channel stride
+  for (int st = 0; st < 5; ++st) {
+    RC(conv1(c, cat, 0, B[B_BRA], 0, c->st_first[st], 256, true));
+    const Act* src = &B[B_BRA];
+    const Act* dst = &B[B_BRB];
+    for (int i = 0; i < 4; ++i) {
+      RC(conv2(c, *src, 0, 128, *dst, 0, 128, c->st_g[st][0][i], c->st_g[st][1][i], 128, 128, true));
+      std::swap(src, dst);
+    }
+    RC(conv2(c, *src, 0, 128, s6, 0, 128, c->st_g[st][0][4], c->st_g[st][1][4], 128, 128, true));
+    RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false));
+  }
+  return OP_OK;
+}
+
+static void post_shape(op_ctx* c, PostShape& s, int n, int lh, int lw, int mh, int mw, double img_len, double sx,
+                       double sy) {
+  s.n = n;
+  s.lh = lh;
+  s.lw = lw;
+  s.mh = mh;
+  s.mw = mw;
+  s.radius = c->gauss_r;
+  s.img_len = img_len;
+  s.sx = sx;
+  s.sy = sy;
+  s.peak_thresh = (float)c->prm.heatmap_peak_thresh;
+  s.n_integ = c->prm.n_integ_points;
+  s.n_integ_thresh = c->prm.n_integ_points_thresh;
+  s.inner_thresh = c->prm.inner_product_thresh;
+  s.len_ratio = c->prm.limb_length_ratio;
+  s.len_penalty = c->prm.length_penalty_value;
+  s.subset_min = c->prm.n_subset_limbs_thresh;
+  s.subset_score = c->prm.subset_score_thresh;
+  memcpy(s.limbs, c->prm.limbs_point, sizeof(s.limbs));
+}
+
+// compute_optimal_size (pose_detector.py:57-73); np.round is half-to-even (nearbyint).
+static void optimal_size(int h, int w, int img_size, int stride, int* out_w, int* out_h) {
+  const double aspect = (double)h / (double)w;
+  int iw, ih;
+  if (h < w) {
+    ih = img_size;
+    iw = (int)std::nearbyint((double)img_size / aspect);
+    const int sur = iw % stride;
+    if (sur) iw += stride - sur;
+  } else {
+    iw = img_size;
+    ih = (int)std::nearbyint((double)img_size * aspect);
+    const int sur = ih % stride;
+    if (sur) ih += stride - sur;
+  }
+  *out_w = iw;
+  *out_h = ih;
+}
+
+static int read_result(op_ctx* c, int frame, double* poses, double* scores, int cap, op_frame_result* res) {
+  int32_t hdr[4];
+  OP_HIP_CHECK(hipMemcpy(hdr, c->pb.res_hdr + 4 * frame, sizeof(hdr), hipMemcpyDeviceToHost));
+  res->status = hdr[0];
+  res->n_peaks = hdr[1];
+  res->n_persons = hdr[2];
+  if (hdr[0] != OP_OK) {
+    set_error(hdr[0] == OP_ERR_INDEX ? "list assignment index out of range (grouping_key_points)"
+                                     : "post-process capacity exceeded (peaks per joint / subsets)");
+    return hdr[0];
+  }
+  if (hdr[2] > cap) {
+    set_error("result capacity too small");
+    return OP_ERR_CAPACITY;
+  }
+  if (hdr[2] > 0) {
+    OP_HIP_CHECK(hipMemcpy(poses, c->pb.res_poses + (size_t)frame * c->pb.maxs * 54, (size_t)hdr[2] * 54 * 8,
+                           hipMemcpyDeviceToHost));
+    OP_HIP_CHECK(hipMemcpy(scores, c->pb.res_scores + (size_t)frame * c->pb.maxs, (size_t)hdr[2] * 8,
+                           hipMemcpyDeviceToHost));
+  }
+  return OP_OK;
+}
+
+static int check_ctx(op_ctx* c, bool need_weights) {
+  if (!c) {
+    set_error("null context");
+    return OP_ERR_INVALID;
+  }
+  if (need_weights && !c->have_weights) {
+    set_error("weights not set (op_set_weights)");
+    return OP_ERR_STATE;
+  }
+  OP_HIP_CHECK(hipSetDevice(c->device));
+  return OP_OK;
+}
+
+}  // namespace op
+
+// =============================== C ABI ===============================
+extern "C" {
+
+const char* op_last_error(void) { return op::g_err.c_str(); }
+
+int op_default_params(op_params* p) {
+  if (!p) return OP_ERR_INVALID;
+  memset(p, 0, sizeof(*p));
+  p->inference_img_size = 368;
+  p->heatmap_size = 320;
+  p->gaussian_sigma = 2.5;
+  p->n_integ_points = 10;
+  p->n_integ_points_thresh = 8;
+  p->heatmap_peak_thresh = 0.05;
+  p->inner_product_thresh = 0.05;
+  p->limb_length_ratio = 1.0;
+  p->length_penalty_value = 1.0;
+  p->n_subset_limbs_thresh = 3;
+  p->subset_score_thresh = 0.2;
+  static const int32_t limbs[OP_N_LIMBS][2] = {{1, 8},  {8, 9},   {9, 10}, {1, 11},  {11, 12}, {12, 13}, {1, 2},
+                                               {2, 3},  {3, 4},   {2, 16}, {1, 5},   {5, 6},   {6, 7},   {5, 17},
+                                               {1, 0},  {0, 14},  {0, 15}, {14, 16}, {15, 17}};
+  memcpy(p->limbs_point, limbs, sizeof(limbs));
+  p->downscale = 8;
+  return OP_OK;
+}
+
+int op_default_limits(op_limits* l) {
+  if (!l) return OP_ERR_INVALID;
+  l->max_batch = 1;
+  l->max_net_h = 368;
+  l->max_net_w = 656;
+  l->max_map_h = 320;
+  l->max_map_w = 576;
+  l->max_peaks_per_joint = 512;
+  l->max_frame_h = 720;
+  l->max_frame_w = 1280;
+  return OP_OK;
+}
+
+int op_layer_info(int index, const char** name, int32_t* ci, int32_t* co, int32_t* ksize) {
+  const auto& L = op::layers();
+  if (index < 0 || index >= (int)L.size()) return OP_ERR_INVALID;
+  if (name) *name = L[index].name;
+  if (ci) *ci = L[index].ci;
+  if (co) *co = L[index].co;
+  if (ksize) *ksize = L[index].k;
+  return OP_OK;
+}
+
+double op_forward_flops(int32_t h, int32_t w) {
+  double f = 0.0;
+  const auto& L = op::layers();
+  for (size_t i = 0; i < L.size(); ++i) {
+    int div = 8;
+    if (i < 2) div = 1;
+    else if (i < 4) div = 2;
+    else if (i < 8) div = 4;
+    const double hw = (double)(h / div) * (double)(w / div);
+    f += 2.0 * L[i].ci * L[i].co * L[i].k * L[i].k * hw;
+  }
+  return f;
+}
+
+int op_create(const op_params* params, const op_limits* limits, int device, op_ctx** out) {
+  if (!out) return OP_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    op::set_error("no HIP device available (this path runs on MI355X only)");
+    return OP_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    op::set_error("device ordinal out of range");
+    return OP_ERR_INVALID;
+  }
+  op_ctx* c = new op_ctx();
+  c->device = device;
+  if (params) c->prm = *params;
+  else op_default_params(&c->prm);
+  op_default_limits(&c->lim);
+  if (limits) {
+    if (limits->max_batch > 0) c->lim.max_batch = limits->max_batch;
+    if (limits->max_net_h > 0) c->lim.max_net_h = limits->max_net_h;
+    if (limits->max_net_w > 0) c->lim.max_net_w = limits->max_net_w;
+    if (limits->max_map_h > 0) c->lim.max_map_h = limits->max_map_h;
+    if (limits->max_map_w > 0) c->lim.max_map_w = limits->max_map_w;
+    if (limits->max_peaks_per_joint > 0) c->lim.max_peaks_per_joint = limits->max_peaks_per_joint;
+    if (limits->max_frame_h > 0) c->lim.max_frame_h = limits->max_frame_h;
+    if (limits->max_frame_w > 0) c->lim.max_frame_w = limits->max_frame_w;
+  }
+  if (c->lim.max_peaks_per_joint > 2048 || c->prm.n_integ_points > 16 || c->prm.n_integ_points < 2) {
+    op::set_error("limits outside kernel support (max_peaks_per_joint <= 2048, 2 <= n_integ_points <= 16)");
+    delete c;
+    return OP_ERR_INVALID;
+  }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    op::set_error("hipStreamCreate failed");
+    delete c;
+    return OP_ERR_HIP;
+  }
+  for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
+  // scipy _gaussian_kernel1d(sigma, 0, int(4*sigma + 0.5)) taps (restated; pinned by the tests)
+  {
+    const double sigma = c->prm.gaussian_sigma;
+    const int r = (int)(4.0 * sigma + 0.5);
+    std::vector<double> w(2 * r + 1);
+    const double coef = -0.5 / (sigma * sigma);
+    for (int i = 0; i <= 2 * r; ++i) w[i] = std::exp(coef * (double)((i - r) * (i - r)));
+    // numpy pairwise sum
+    const int n = 2 * r + 1;
+    double s;
+    if (n < 8) {
+      s = 0;
+      for (int i = 0; i < n; ++i) s += w[i];
+    } else {
+      double rr[8];
+      for (int j = 0; j < 8; ++j) rr[j] = w[j];
+      int i = 8;
+      for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) rr[j] += w[i + j];
+      s = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+      for (; i < n; ++i) s += w[i];
+    }
+    for (auto& v : w) v = v / s;
+    c->gauss_host = w;
+    c->gauss_r = r;
+  }
+  *out = c;
+  return OP_OK;
+}
+
+static void free_pc(op::PackedConv& p) {
+  if (p.w) hipFree(p.w);
+  if (p.b) hipFree(p.b);
+  p.w = p.b = nullptr;
+}
+
+static void free_weights(op_ctx* c) {
+  for (auto& p : c->bb) free_pc(p);
+  free_pc(c->s1_first);
+  for (auto& a : c->s1_g)
+    for (auto& p : a) free_pc(p);
+  for (auto& p : c->s1_last) free_pc(p);
+  for (auto& p : c->st_first) free_pc(p);
+  for (auto& a : c->st_g)
+    for (auto& b : a)
+      for (auto& p : b) free_pc(p);
+  for (auto& a : c->st_last)
+    for (auto& p : a) free_pc(p);
+  c->have_weights = false;
+}
+
+int op_destroy(op_ctx* c) {
+  if (!c) return OP_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->gexec) hipGraphExecDestroy(c->gexec);
+  if (c->graph) hipGraphDestroy(c->graph);
+  free_weights(c);
+  if (c->arena) hipFree(c->arena);
+  if (c->post_arena) hipFree(c->post_arena);
+  if (c->d_frames) hipFree(c->d_frames);
+  if (c->d_maps) hipFree(c->d_maps);
+  if (c->d_scratch) hipFree(c->d_scratch);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  for (auto& e : c->ev_pool) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return OP_OK;
+}
+
+int op_set_weights(op_ctx* c, const float* const* W, const float* const* b) {
+  using namespace op;
+  int rc = check_ctx(c, false);
+  if (rc) return rc;
+  if (!W || !b) {
+    set_error("null weights");
+    return OP_ERR_INVALID;
+  }
+  for (int i = 0; i < OP_N_LAYERS; ++i)
+    if (!W[i] || !b[i]) {
+      set_error(std::string("missing weights for layer ") + layers()[i].name);
+      return OP_ERR_INVALID;
+    }
+  free_weights(c);
+  const auto& L = layers();
+  auto single = [&](PackedConv& pc, int li, bool cat_in) -> int {
+    const LayerDef& d = L[li];
+    pc.ks = d.k;
+    pc.cin_phys = cat_in ? kCatStride : round_up(d.ci, 8);
+    pc.cop = round_up(d.co, 64);
+    pc.cin_log = d.ci;
+    pc.co_log = d.co;
+    std::vector<float> w((size_t)pc.cin_phys * d.k * d.k * pc.cop, 0.0f), bias(pc.cop, 0.0f);
+    pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[li], b[li], d.co, d.ci, 0, cat_in);
+    return upload(pc, w, bias);
+  };
+  auto fused = [&](PackedConv& pc, int l1, int l2, bool cat_in) -> int {
+    const LayerDef& d = L[l1];
+    pc.ks = d.k;
+    pc.cin_phys = cat_in ? kCatStride : round_up(d.ci, 8);
+    pc.cop = 2 * d.co;
+    pc.cin_log = d.ci;
+    pc.co_log = 2 * d.co;
+    std::vector<float> w((size_t)pc.cin_phys * d.k * d.k * pc.cop, 0.0f), bias(pc.cop, 0.0f);
+    pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[l1], b[l1], d.co, d.ci, 0, cat_in);
+    pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[l2], b[l2], d.co, d.ci, d.co, cat_in);
+    return upload(pc, w, bias);
+  };
+  for (int i = 0; i < 12; ++i) RC(single(c->bb[i], i, false));
+  const char* br[2] = {"L1", "L2"};
+  RC(fused(c->s1_first, layer_index("conv5_1_CPM_L1"), layer_index("conv5_1_CPM_L2"), false));
+  for (int bi = 0; bi < 2; ++bi) {
+    for (int k = 0; k < 3; ++k)
+      RC(single(c->s1_g[bi][k], layer_index("conv5_" + std::to_string(k + 2) + "_CPM_" + br[bi]), false));
+    RC(single(c->s1_last[bi], layer_index(std::string("conv5_5_CPM_") + br[bi]), false));
+  }
+  for (int s = 0; s < 5; ++s) {
+    const std::string st = "_stage" + std::to_string(s + 2) + "_";
+    RC(fused(c->st_first[s], layer_index("Mconv1" + st + "L1"), layer_index("Mconv1" + st + "L2"), true));
+    for (int bi = 0; bi < 2; ++bi) {
+      for (int k = 0; k < 5; ++k) RC(single(c->st_g[s][bi][k], layer_index("Mconv" + std::to_string(k + 2) + st + br[bi]), false));
+      RC(single(c->st_last[s][bi], layer_index("Mconv7" + st + br[bi]), false));
+    }
+  }
+  c->have_weights = true;
+  return OP_OK;
+}
+
+int op_preprocess(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, int32_t out_w,
+                  int32_t out_h, float* x_out) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!bgr || !x_out || h < 1 || w < 1 || out_w < 1 || out_h < 1 || row_stride < (int64_t)w * 3) {
+    set_error("op_preprocess: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const size_t in_bytes = (size_t)h * w * 3, out_bytes = (size_t)3 * out_h * out_w * 4;
+  RC(ensure_scratch(c, in_bytes + 256 + out_bytes));
+  uint8_t* din = (uint8_t*)c->d_scratch;
+  float* dout = (float*)((char*)c->d_scratch + (in_bytes + 255) / 256 * 256);
+  OP_HIP_CHECK(hipMemcpy2DAsync(din, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h, hipMemcpyHostToDevice,
+                                c->stream));
+  RC(launch_preprocess_planar(din, (int64_t)w * 3, h, w, out_h, out_w, dout, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(x_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+int op_forward(op_ctx* c, const float* x, int32_t n, int32_t h, int32_t w, float* pafs, float* heatmaps) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (!x || !pafs || !heatmaps) {
+    set_error("op_forward: null pointer");
+    return OP_ERR_INVALID;
+  }
+  RC(ensure_geometry(c, n, h, w));
+  const size_t xin = (size_t)n * 3 * h * w * 4;
+  const int lh = h / 8, lw = w / 8;
+  const size_t outb = (size_t)n * 57 * lh * lw * 4;
+  RC(ensure_scratch(c, xin + 256 + outb));
+  float* dx = c->d_scratch;
+  float* dmaps = (float*)((char*)c->d_scratch + (xin + 255) / 256 * 256);
+  OP_HIP_CHECK(hipMemcpyAsync(dx, x, xin, hipMemcpyHostToDevice, c->stream));
+  RC(launch_nchw_to_nhwc8(dx, c->buf[B_X0].p, n, h, w, c->stream));
+  RC(run_forward(c));
+  float* dpaf = dmaps;
+  float* dheat = dmaps + (size_t)n * 38 * lh * lw;
+  RC(launch_extract_maps(c->buf[B_CAT].p, n, lh, lw, dpaf, dheat, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(pafs, dpaf, (size_t)n * 38 * lh * lw * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(heatmaps, dheat, (size_t)n * 19 * lh * lw * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+int op_resize_images(op_ctx* c, const float* x, int32_t ch, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!x || !y || ch < 1 || h < 2 || w < 2 || oh < 1 || ow < 1) {
+    set_error("op_resize_images: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const size_t inb = (size_t)ch * h * w * 4, outb = (size_t)ch * oh * ow * 4;
+  RC(ensure_scratch(c, inb + 256 + outb));
+  float* din = c->d_scratch;
+  float* dout = (float*)((char*)c->d_scratch + (inb + 255) / 256 * 256);
+  OP_HIP_CHECK(hipMemcpyAsync(din, x, inb, hipMemcpyHostToDevice, c->stream));
+  RC(launch_resize_images(din, ch, h, w, oh, ow, dout, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(y, dout, outb, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+// Upload (N,5) all_peaks rows (reference format: ordered by joint, ids = row index) into the
+// per-joint peak arrays of frame 0.
+static int upload_peaks(op_ctx* c, const double* peaks, int64_t n) {
+  using namespace op;
+  const int maxp = c->pb.maxp;
+  std::vector<int32_t> xy((size_t)OP_N_JOINTS * maxp, 0), cnt(OP_N_JOINTS, 0);
+  std::vector<float> sc((size_t)OP_N_JOINTS * maxp, 0.0f);
+  int prev = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const double* r = peaks + i * 5;
+    const int j = (int)r[0];
+    if (j < 0 || j >= OP_N_JOINTS || j < prev || (int64_t)r[4] != i || r[1] < 0 || r[2] < 0 || r[1] > 0xffff ||
+        r[2] > 0x7fff) {
+      set_error("peaks must be all_peaks rows [joint, x, y, score, id] ordered by joint with id = row");
+      return OP_ERR_INVALID;
+    }
+    prev = j;
+    if (cnt[j] >= maxp) {
+      set_error("too many peaks for one joint (max_peaks_per_joint)");
+      return OP_ERR_CAPACITY;
+    }
+    xy[(size_t)j * maxp + cnt[j]] = (int32_t)r[1] | ((int32_t)r[2] << 16);
+    sc[(size_t)j * maxp + cnt[j]] = (float)r[3];
+    cnt[j]++;
+  }
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_xy, xy.data(), xy.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_score, sc.data(), sc.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+int op_compute_peaks(op_ctx* c, const float* heatmaps, int32_t ch, int32_t h, int32_t w, double* peaks, int64_t cap,
+                     int64_t* n_peaks) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!heatmaps || !n_peaks || ch != OP_N_JOINTS + 1 || h < 2 || w < 2) {
+    set_error("op_compute_peaks: heatmaps must be (19, h, w)");
+    return OP_ERR_INVALID;
+  }
+  RC(ensure_post(c, 1, h, w));
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.up, heatmaps, (size_t)OP_N_JOINTS * h * w * 4, hipMemcpyHostToDevice, c->stream));
+  PostShape s;
+  post_shape(c, s, 1, h, w, h, w, (double)w, 1.0, 1.0);
+  RC(launch_peaks_from_full(c->pb.up, OP_N_JOINTS, h, w, s, c->pb, c->stream));
+  const int maxp = c->pb.maxp;
+  std::vector<int32_t> cnt(OP_N_JOINTS), xy((size_t)OP_N_JOINTS * maxp);
+  std::vector<float> sc((size_t)OP_N_JOINTS * maxp);
+  OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), c->pb.peak_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(xy.data(), c->pb.peak_xy, xy.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), c->pb.peak_score, sc.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  int64_t k = 0;
+  for (int j = 0; j < OP_N_JOINTS; ++j) {
+    if (cnt[j] > maxp) {
+      set_error("too many peaks for one joint (max_peaks_per_joint)");
+      return OP_ERR_CAPACITY;
+    }
+    for (int i = 0; i < cnt[j]; ++i) {
+      if (k >= cap) {
+        set_error("peaks capacity too small");
+        return OP_ERR_CAPACITY;
+      }
+      const int32_t v = xy[(size_t)j * maxp + i];
+      double* r = peaks + k * 5;
+      r[0] = j;
+      r[1] = v & 0xffff;
+      r[2] = v >> 16;
+      r[3] = (double)sc[(size_t)j * maxp + i];
+      r[4] = (double)k;
+      ++k;
+    }
+  }
+  *n_peaks = k;
+  return OP_OK;
+}
+
+int op_compute_connections(op_ctx* c, const float* pafs, int32_t h, int32_t w, const double* peaks, int64_t n_peaks,
+                           double img_len, double* conn, int64_t cap, int64_t* conn_off) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!pafs || !conn_off || (n_peaks > 0 && !peaks) || h < 1 || w < 1) {
+    set_error("op_compute_connections: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  RC(ensure_post(c, 1, h, w));
+  RC(upload_peaks(c, peaks, n_peaks));
+  const size_t pb = (size_t)OP_N_PAF * h * w * 4;
+  RC(ensure_scratch(c, pb));
+  OP_HIP_CHECK(hipMemcpyAsync(c->d_scratch, pafs, pb, hipMemcpyHostToDevice, c->stream));
+  PostShape s;
+  post_shape(c, s, 1, h, w, h, w, img_len, 1.0, 1.0);
+  RC(launch_connections_full(c->d_scratch, h, w, s, c->pb, c->stream));
+  const int maxp = c->pb.maxp;
+  std::vector<int32_t> cnt(OP_N_LIMBS), ab((size_t)OP_N_LIMBS * maxp * 2), ccnt(OP_N_LIMBS);
+  std::vector<double> sc((size_t)OP_N_LIMBS * maxp);
+  OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), c->pb.conn_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(ccnt.data(), c->pb.cand_cnt, ccnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(ab.data(), c->pb.conn_ab, ab.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), c->pb.conn_score, sc.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  int64_t k = 0;
+  for (int l = 0; l < OP_N_LIMBS; ++l) {
+    if (ccnt[l] > c->pb.maxc) {
+      set_error("candidate capacity exceeded");
+      return OP_ERR_CAPACITY;
+    }
+    conn_off[l] = k;
+    for (int i = 0; i < cnt[l]; ++i) {
+      if (k >= cap) {
+        set_error("connection capacity too small");
+        return OP_ERR_CAPACITY;
+      }
+      conn[k * 3 + 0] = ab[((size_t)l * maxp + i) * 2];
+      conn[k * 3 + 1] = ab[((size_t)l * maxp + i) * 2 + 1];
+      conn[k * 3 + 2] = sc[(size_t)l * maxp + i];
+      ++k;
+    }
+  }
+  conn_off[OP_N_LIMBS] = k;
+  return OP_OK;
+}
+
+int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const double* peaks, int64_t n_peaks,
+                double* subsets, int64_t cap, int64_t* n_subsets) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!conn_off || !n_subsets || (n_peaks > 0 && !peaks)) {
+    set_error("op_grouping: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  // map size is irrelevant for grouping; keep whatever post buffers exist
+  RC(ensure_post(c, 1, std::max(c->pmh, 8), std::max(c->pmw, 8)));
+  RC(upload_peaks(c, peaks, n_peaks));
+  const int maxp = c->pb.maxp;
+  std::vector<int32_t> cnt(OP_N_LIMBS, 0), ab((size_t)OP_N_LIMBS * maxp * 2, 0);
+  std::vector<double> sc((size_t)OP_N_LIMBS * maxp, 0.0);
+  // peak id ranges per joint (ids are row indices of all_peaks, grouped by joint)
+  int64_t jlo[OP_N_JOINTS], jhi[OP_N_JOINTS];
+  for (int j = 0; j < OP_N_JOINTS; ++j) {
+    jlo[j] = 0;
+    jhi[j] = -1;
+  }
+  for (int64_t i = n_peaks - 1; i >= 0; --i) jlo[(int)peaks[i * 5]] = i;
+  for (int64_t i = 0; i < n_peaks; ++i) jhi[(int)peaks[i * 5]] = i;
+  for (int l = 0; l < OP_N_LIMBS; ++l) {
+    const int64_t k0 = conn_off[l], k1 = conn_off[l + 1];
+    if (k1 - k0 > maxp || k1 < k0) {
+      set_error("too many connections for one limb");
+      return OP_ERR_CAPACITY;
+    }
+    const int ja = c->prm.limbs_point[l][0], jb = c->prm.limbs_point[l][1];
+    for (int64_t i = k0; i < k1; ++i) {
+      const int64_t ia = (int64_t)conn[i * 3], ib = (int64_t)conn[i * 3 + 1];
+      if (ia < jlo[ja] || ia > jhi[ja] || ib < jlo[jb] || ib > jhi[jb]) {
+        set_error("connection ids do not belong to the limb's joints");
+        return OP_ERR_INVALID;
+      }
+    }
+    cnt[l] = (int)(k1 - k0);
+    for (int64_t i = k0; i < k1; ++i) {
+      ab[((size_t)l * maxp + (i - k0)) * 2] = (int32_t)conn[i * 3];
+      ab[((size_t)l * maxp + (i - k0)) * 2 + 1] = (int32_t)conn[i * 3 + 1];
+      sc[(size_t)l * maxp + (i - k0)] = conn[i * 3 + 2];
+    }
+  }
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_ab, ab.data(), ab.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_score, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, c->stream));
+  PostShape s;
+  post_shape(c, s, 1, 8, 8, 8, 8, 8.0, 1.0, 1.0);
+  RC(launch_grouping(s, c->pb, c->stream));
+  int32_t hdr[4];
+  OP_HIP_CHECK(hipMemcpyAsync(hdr, c->pb.res_hdr, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (hdr[0] == OP_ERR_INDEX) {
+    set_error("list assignment index out of range (grouping_key_points)");
+    return OP_ERR_INDEX;
+  }
+  if (hdr[0] != OP_OK) {
+    set_error("grouping capacity exceeded");
+    return hdr[0];
+  }
+  if (hdr[2] > cap) {
+    set_error("subsets capacity too small");
+    return OP_ERR_CAPACITY;
+  }
+  if (hdr[2] > 0)
+    OP_HIP_CHECK(hipMemcpy(subsets, c->pb.res_subsets, (size_t)hdr[2] * 20 * 8, hipMemcpyDeviceToHost));
+  *n_subsets = hdr[2];
+  return OP_OK;
+}
+
+// Pack planar (n, 57, lh, lw) maps [38 paf | 19 heat] into an NHWC (n, lh, lw, 57) device buffer.
+static int stage_maps_dev(op_ctx* c, const float* maps, int n, int lh, int lw, float** out) {
+  using namespace op;
+  const size_t fl = (size_t)n * 57 * lh * lw;
+  std::vector<float> t(fl);
+  for (int f = 0; f < n; ++f)
+    for (int ch = 0; ch < 57; ++ch)
+      for (int y = 0; y < lh; ++y)
+        for (int x = 0; x < lw; ++x)
+          t[(((size_t)f * lh + y) * lw + x) * 57 + ch] = maps[(((size_t)f * 57 + ch) * lh + y) * lw + x];
+  if (fl * 4 > c->maps_bytes) {
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (c->d_maps) OP_HIP_CHECK(hipFree(c->d_maps));
+    c->d_maps = nullptr;
+    OP_HIP_CHECK(hipMalloc(&c->d_maps, fl * 4));
+    c->maps_bytes = fl * 4;
+  }
+  OP_HIP_CHECK(hipMemcpy(c->d_maps, t.data(), fl * 4, hipMemcpyHostToDevice));
+  *out = c->d_maps;
+  return OP_OK;
+}
+
+int op_postprocess(op_ctx* c, const float* paf_low, const float* heat_low, int32_t h, int32_t w, int32_t orig_h,
+                   int32_t orig_w, double* poses, double* scores, int32_t cap, op_frame_result* res) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!paf_low || !heat_low || !res || h < 2 || w < 2 || orig_h < 1 || orig_w < 1) {
+    set_error("op_postprocess: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  std::vector<float> maps((size_t)57 * h * w);
+  memcpy(maps.data(), paf_low, (size_t)38 * h * w * 4);
+  memcpy(maps.data() + (size_t)38 * h * w, heat_low, (size_t)19 * h * w * 4);
+  float* dm = nullptr;
+  RC(stage_maps_dev(c, maps.data(), 1, h, w, &dm));
+  int map_w, map_h;
+  optimal_size(orig_h, orig_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  RC(ensure_post(c, 1, map_h, map_w));
+  MapSource src{dm, (int64_t)57 * h * w, 0, 57, 0, 38};
+  PostShape s;
+  post_shape(c, s, 1, h, w, map_h, map_w, (double)map_w, (double)orig_w / map_w, (double)orig_h / map_h);
+  RC(launch_post_maps(src, s, c->pb, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  memset(res, 0, sizeof(*res));
+  res->map_w = map_w;
+  res->map_h = map_h;
+  return read_result(c, 0, poses, scores, cap, res);
+}
+
+// Enqueue preprocess + forward + post-process for the staged batch on the context stream.
+static int enqueue_staged(op_ctx* c, bool timing) {
+  using namespace op;
+  int in_w, in_h, map_w, map_h;
+  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
+  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  RC(ensure_geometry(c, c->st_n, in_h, in_w));
+  RC(ensure_post(c, c->st_n, map_h, map_w));
+  if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[0], c->stream));
+  RC(launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h, c->st_w,
+                       in_h, in_w, c->buf[B_X0].p, c->stream));
+  RC(run_forward(c));
+  if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[1], c->stream));
+  const int lh = in_h / 8, lw = in_w / 8;
+  MapSource src;
+  if (c->use_maps) {
+    if (c->sm_n < c->st_n || c->sm_h != lh || c->sm_w != lw) {
+      set_error("staged maps do not match the staged frames (n, h/8, w/8)");
+      return OP_ERR_STATE;
+    }
+    src = MapSource{c->d_maps, (int64_t)57 * lh * lw, 0, 57, 0, 38};
+  } else {
+    const Act& cat = c->buf[B_CAT];
+    src = MapSource{cat.p, (int64_t)cat.frame_floats(), cat.pad, cat.cs, kCatPaf, kCatHeat};
+  }
+  PostShape s;
+  post_shape(c, s, c->st_n, lh, lw, map_h, map_w, (double)map_w, (double)c->st_w / map_w, (double)c->st_h / map_h);
+  // post-process algorithmic HBM bytes: 57-ch low-res read + 18-ch upsample write +
+  // 2 x (read + write) Gaussian passes + NMS read, f32
+  const double mp = (double)c->st_n * map_h * map_w;
+  const double pbytes = 4.0 * ((double)c->st_n * 57 * lh * lw + 18 * mp + 2 * 2 * 18 * mp + 18 * mp);
+  RC(profiled(c, 3, 0.0, pbytes, [&] { return launch_post_maps(src, s, c->pb, c->stream); }));
+  if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[2], c->stream));
+  c->timed = timing;
+  return OP_OK;
+}
+
+int op_stage_frames(op_ctx* c, const uint8_t* frames, int32_t n, int32_t h, int32_t w) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!frames || n < 1 || h < 8 || w < 8) {
+    set_error("op_stage_frames: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const size_t bytes = (size_t)n * h * w * 3;
+  if (bytes > c->frames_bytes) {
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (c->d_frames) OP_HIP_CHECK(hipFree(c->d_frames));
+    c->d_frames = nullptr;
+    OP_HIP_CHECK(hipMalloc(&c->d_frames, bytes));
+    c->frames_bytes = bytes;
+  }
+  OP_HIP_CHECK(hipMemcpyAsync(c->d_frames, frames, bytes, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->st_n != n || c->st_h != h || c->st_w != w) {
+    if (c->gexec) {
+      hipGraphExecDestroy(c->gexec);
+      c->gexec = nullptr;
+    }
+  }
+  c->st_n = n;
+  c->st_h = h;
+  c->st_w = w;
+  return OP_OK;
+}
+
+int op_stage_maps(op_ctx* c, const float* maps, int32_t n, int32_t mh, int32_t mw) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!maps || n < 1 || mh < 2 || mw < 2) {
+    set_error("op_stage_maps: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  float* dm;
+  RC(stage_maps_dev(c, maps, n, mh, mw, &dm));
+  c->sm_n = n;
+  c->sm_h = mh;
+  c->sm_w = mw;
+  if (c->gexec) {
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  return OP_OK;
+}
+
+int op_use_staged_maps(op_ctx* c, int32_t enable) {
+  if (!c) return OP_ERR_INVALID;
+  c->use_maps = enable != 0;
+  if (c->gexec) {
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  return OP_OK;
+}
+
+int op_run_staged(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (c->st_n < 1) {
+    set_error("no staged frames");
+    return OP_ERR_STATE;
+  }
+  return enqueue_staged(c, true);
+}
+
+int op_run_staged_graph(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (c->st_n < 1) {
+    set_error("no staged frames");
+    return OP_ERR_STATE;
+  }
+  // geometry/buffers must exist before capture (allocation and memsets are not captured)
+  int in_w, in_h, map_w, map_h;
+  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
+  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  RC(ensure_geometry(c, c->st_n, in_h, in_w));
+  RC(ensure_post(c, c->st_n, map_h, map_w));
+  // the graph bakes in every pointer and size: replay only if none changed since capture
+  const uintptr_t key[10] = {(uintptr_t)c->st_n, (uintptr_t)c->st_h, (uintptr_t)c->st_w, (uintptr_t)c->use_maps,
+                             (uintptr_t)c->arena, (uintptr_t)c->post_arena, (uintptr_t)c->d_frames,
+                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw)};
+  if (c->gexec && memcmp(key, c->g_key, sizeof(key)) != 0) {
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  if (!c->gexec) {
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    memcpy(c->g_key, key, sizeof(key));
+    const bool prof = c->prof;
+    c->prof = false;  // no event records inside the capture
+    if (c->graph) {
+      hipGraphDestroy(c->graph);
+      c->graph = nullptr;
+    }
+    OP_HIP_CHECK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_staged(c, false);
+    c->prof = prof;
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc) {
+      if (g) hipGraphDestroy(g);
+      return rc;
+    }
+    OP_HIP_CHECK(e);
+    c->graph = g;
+    OP_HIP_CHECK(hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
+  }
+  OP_HIP_CHECK(hipGraphLaunch(c->gexec, c->stream));
+  c->timed = false;
+  return OP_OK;
+}
+
+int op_synchronize(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+int op_fetch_result(op_ctx* c, int32_t frame, double* poses, double* scores, int32_t cap, op_frame_result* res) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!res || frame < 0 || frame >= c->st_n) {
+    set_error("op_fetch_result: bad frame");
+    return OP_ERR_INVALID;
+  }
+  memset(res, 0, sizeof(*res));
+  int in_w, in_h, map_w, map_h;
+  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
+  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  res->map_w = map_w;
+  res->map_h = map_h;
+  res->net_w = in_w;
+  res->net_h = in_h;
+  return read_result(c, frame, poses, scores, cap, res);
+}
+
+int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, double* poses, double* scores,
+              int32_t cap, op_frame_result* res) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (!bgr || !res || h < 8 || w < 8 || row_stride < (int64_t)w * 3) {
+    set_error("op_detect: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const size_t bytes = (size_t)h * w * 3;
+  if (bytes > c->frames_bytes) {
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (c->d_frames) OP_HIP_CHECK(hipFree(c->d_frames));
+    c->d_frames = nullptr;
+    OP_HIP_CHECK(hipMalloc(&c->d_frames, bytes));
+    c->frames_bytes = bytes;
+  }
+  OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
+                                hipMemcpyHostToDevice, c->stream));
+  c->st_n = 1;
+  c->st_h = h;
+  c->st_w = w;
+  const bool keep_maps = c->use_maps;
+  c->use_maps = false;
+  int rc = enqueue_staged(c, false);
+  c->use_maps = keep_maps;
+  if (rc) return rc;
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return op_fetch_result(c, 0, poses, scores, cap, res);
+}
+
+int op_profile_enable(op_ctx* c, int32_t enable) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  c->prof = enable != 0;
+  return OP_OK;
+}
+
+int op_profile_reset(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  c->pending.clear();
+  c->ev_used = 0;
+  for (int i = 0; i < 4; ++i) {
+    c->prof_ms[i] = c->prof_flops[i] = c->prof_bytes[i] = 0.0;
+    c->prof_n[i] = 0;
+  }
+  return OP_OK;
+}
+
+int op_profile_read(op_ctx* c, int32_t cls, double* ms, int64_t* launches, double* flops, double* bytes) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (cls < 0 || cls > 3) {
+    set_error("profile class must be 0..3");
+    return OP_ERR_INVALID;
+  }
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  for (const ProfPair& p : c->pending) {
+    float t = 0.0f;
+    OP_HIP_CHECK(hipEventElapsedTime(&t, p.a, p.b));
+    c->prof_ms[p.cls] += t;
+    c->prof_n[p.cls] += 1;
+    c->prof_flops[p.cls] += p.flops;
+    c->prof_bytes[p.cls] += p.bytes;
+  }
+  c->pending.clear();
+  c->ev_used = 0;
+  if (ms) *ms = c->prof_ms[cls];
+  if (launches) *launches = c->prof_n[cls];
+  if (flops) *flops = c->prof_flops[cls];
+  if (bytes) *bytes = c->prof_bytes[cls];
+  return OP_OK;
+}
+
+int op_last_timing(op_ctx* c, double* conv_ms, double* post_ms, double* total_ms) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!c->timed) {
+    set_error("no timed run (use op_run_staged)");
+    return OP_ERR_STATE;
+  }
+  OP_HIP_CHECK(hipEventSynchronize(c->ev[2]));
+  float a = 0, b = 0;
+  OP_HIP_CHECK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+  OP_HIP_CHECK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+  if (conv_ms) *conv_ms = a;
+  if (post_ms) *post_ms = b;
+  if (total_ms) *total_ms = (double)a + b;
+  return OP_OK;
+}
+
+}  // extern "C"

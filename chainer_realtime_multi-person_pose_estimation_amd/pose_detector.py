@@ -1,0 +1,133 @@
+"""``PoseDetector`` — drop-in for the reference's detector (pose_detector.py:15-517), MI355X only.
+
+Same constructor and call signature, same return types and empty-result shapes.  Each method
+named after a reference method runs that step through the HIP library (C ABI in
+include/openpose_hip.h); ``__call__`` runs the whole path on the device in one call
+(resize + normalise, 92 convs, upsample, Gaussian + NMS, line integrals, greedy assignment,
+grouping) and only the final poses come back to the host.
+
+There is no CPU path: ``device=-1`` (the reference's CPU default) selects HIP device 0.
+"""
+import numpy as np
+
+from . import _lib
+from . import weights as _weights
+from .constants import JointType, params
+
+
+class PoseDetector(object):
+    """PoseDetector(arch=None, weights_file=None, model=None, device=-1, precise=False)
+
+    arch: 'posenet' (the CocoPoseNet path; entity.py:50-54).
+    weights_file: Chainer npz written by serializers.save_npz (pose_detector.py:26).
+    model: instead of a file, a {layer: (W, b)} dict (e.g. weights.random_weights()); like the
+           reference's ``model=`` it skips loading from disk.
+    device: HIP device ordinal (negative -> 0).
+    precise: multi-scale inference (pose_detector.py:433-482).
+    """
+
+    def __init__(self, arch=None, weights_file=None, model=None, device=-1, precise=False, max_batch=1):
+        self.arch = arch
+        self.precise = precise
+        if model is None and arch not in (None, "posenet"):
+            raise ValueError("arch %r is not on this path (only 'posenet')" % (arch,))
+        self.device = 0 if device is None or device < 0 else int(device)
+        limits = _lib.OpLimits()
+        limits.max_batch = int(max_batch)
+        self._ctx = _lib.Context(self.device, _lib.params_from_dict(params), limits)
+        if model is not None:
+            w = model
+        elif weights_file:
+            print("Loading the model...")
+            w = _weights.load_npz(weights_file)
+        else:
+            print("Loading the model...")
+            w = _weights.random_weights(0)
+        self._ctx.set_weights(w)
+
+    # ---- helpers mirrored from the reference (host-side arithmetic only) ----
+    def create_gaussian_kernel(self, sigma=1, ksize=5):
+        """pose_detector.py:38-44 (the reference's GPU-branch kernel; kept for API parity)."""
+        center = int(ksize / 2)
+        d2 = (np.arange(ksize)[None, :] - center) ** 2 + (np.arange(ksize)[:, None] - center) ** 2
+        return (np.exp(-0.5 * d2 / sigma ** 2) / (sigma ** 2 * 2 * np.pi)).astype("f")
+
+    def pad_image(self, img, stride, pad_value):
+        """pose_detector.py:46-55: pad bottom/right to a multiple of stride with pad_value."""
+        h, w, _ = img.shape
+        pad = [(stride - (h % stride)) % stride, (stride - (w % stride)) % stride]
+        out = np.empty((h + pad[0], w + pad[1], 3), "uint8")
+        out[...] = np.asarray(pad_value, dtype=np.int64).astype("uint8")
+        out[:h, :w, :] = img
+        return out, pad
+
+    def compute_optimal_size(self, orig_img, img_size, stride=8):
+        """pose_detector.py:57-73: (w, h) with the short side = img_size, multiples of stride."""
+        h, w = orig_img.shape[:2]
+        aspect = h / w
+        if h < w:
+            sh, sw = img_size, int(np.round(img_size / aspect))
+            sw += (stride - sw % stride) % stride
+        else:
+            sw, sh = img_size, int(np.round(img_size * aspect))
+            sh += (stride - sh % stride) % stride
+        return sw, sh
+
+    def preprocess(self, img):
+        """pose_detector.py:426-431 (x/255 - 0.5, HWC -> 1x3xHxW, BGR kept)."""
+        x = img.astype("f")
+        x /= 255
+        x -= 0.5
+        return x.transpose(2, 0, 1)[None]
+
+    # ---- hot-path steps on the device ----
+    def compute_peaks_from_heatmaps(self, heatmaps):
+        """pose_detector.py:75-110 (CPU semantics): (19,H,W) -> all_peaks (N,5) or array([])."""
+        peaks = self._ctx.compute_peaks(np.asarray(heatmaps, np.float32))
+        return peaks if len(peaks) else np.array([])
+
+    def compute_connections(self, pafs, all_peaks, img_len, params):
+        """pose_detector.py:161-181 -> list of 19 (K,3) f64 arrays."""
+        self._check_params(params)
+        return self._ctx.compute_connections(np.asarray(pafs, np.float32), all_peaks, img_len)
+
+    def grouping_key_points(self, all_connections, candidate_peaks, params):
+        """pose_detector.py:183-250 -> (S,20) f64 subsets (raises IndexError like the reference)."""
+        self._check_params(params)
+        return self._ctx.grouping(all_connections, candidate_peaks)
+
+    def subsets_to_pose_array(self, subsets, all_peaks):
+        """pose_detector.py:252-265."""
+        rows = []
+        for subset in subsets:
+            ids = subset[:len(JointType)].astype("i")
+            pose = np.zeros((len(JointType), 3))
+            have = ids >= 0
+            pose[have, :2] = all_peaks[ids[have]][:, 1:3]
+            pose[have, 2] = 2
+            rows.append(pose)
+        return np.array(rows)
+
+    def _check_params(self, p):
+        if p is not params:
+            for k in ("n_integ_points", "n_integ_points_thresh", "inner_product_thresh", "limb_length_ratio",
+                      "length_penalty_value", "n_subset_limbs_thresh", "subset_score_thresh"):
+                if p.get(k) != params[k]:
+                    raise ValueError("params[%r] differs from the context's; build a new PoseDetector" % k)
+
+    def detect_precise(self, orig_img):
+        raise NotImplementedError("precise (multi-scale) inference is not built yet on this path")
+
+    def __call__(self, orig_img):
+        """pose_detector.py:484-517: BGR uint8 image -> (poses (P,18,3) f64, scores (P,) f64)."""
+        if self.precise:
+            return self.detect_precise(orig_img)
+        img = np.asarray(orig_img)
+        if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        poses, scores, res = self._ctx.detect(img)
+        if res.n_peaks == 0:
+            return np.empty((0, len(JointType), 3)), np.empty(0)
+        if res.n_persons == 0:
+            return np.array([]), np.empty(0)
+        return poses, scores

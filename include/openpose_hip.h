@@ -1,0 +1,164 @@
+/*
+ * openpose_hip.h — C ABI of the MI355X (gfx950) OpenPose inference path.
+ *
+ * Drop-in replacement for the hot path of nk35jk/Chainer_Realtime_Multi-Person_Pose_Estimation:
+ * PoseDetector.__call__ (pose_detector.py:484-517) = CocoPoseNet forward
+ * (models/CocoPoseNet.py:132-262) + PAF post-process (pose_detector.py:75-265).
+ * The reference has no FFI of its own (pure Python); every entry point below names the
+ * reference function it replaces.  The Python host package
+ * (chainer_realtime_multi-person_pose_estimation_amd/) binds these with ctypes.
+ *
+ * Conventions: plain pointers + sizes; all host pointers, row-major, C-contiguous.
+ * Every function returns an int status (OP_OK = 0); op_last_error() describes the last failure
+ * on the calling thread.  A context is single-threaded and owns one HIP stream on one device.
+ */
+#ifndef OPENPOSE_HIP_H
+#define OPENPOSE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OP_OK 0
+#define OP_ERR_INVALID 1  /* bad argument / shape */
+#define OP_ERR_HIP 2      /* HIP runtime failure */
+#define OP_ERR_CAPACITY 3 /* a per-frame cap (peaks/persons) was exceeded */
+#define OP_ERR_INDEX 4    /* reference raises IndexError (pose_detector.py:197): a connection hit >=3 subsets */
+#define OP_ERR_STATE 5    /* weights not set / no staged frames */
+
+#define OP_N_JOINTS 18 /* JointType, entity.py:9-46 */
+#define OP_N_LIMBS 19  /* params['limbs_point'], entity.py:85-105 */
+#define OP_N_PAF 38
+#define OP_N_HEAT 19
+#define OP_N_LAYERS 92 /* models/CocoPoseNet.py:26-129 */
+
+/* Inference parameters — entity.py:70-105 (same names and meaning). */
+typedef struct op_params {
+  int32_t inference_img_size;   /* 368 */
+  int32_t heatmap_size;         /* 320 */
+  double gaussian_sigma;        /* 2.5 (scipy gaussian_filter, truncate 4.0) */
+  int32_t n_integ_points;       /* 10 */
+  int32_t n_integ_points_thresh;/* 8 */
+  double heatmap_peak_thresh;   /* 0.05 */
+  double inner_product_thresh;  /* 0.05 */
+  double limb_length_ratio;     /* 1.0 */
+  double length_penalty_value;  /* 1 */
+  int32_t n_subset_limbs_thresh;/* 3 */
+  double subset_score_thresh;   /* 0.2 */
+  int32_t limbs_point[OP_N_LIMBS][2];
+  int32_t downscale;            /* 8 */
+} op_params;
+
+/* Capacities of a context (device buffers are sized from these; 0 = default). */
+typedef struct op_limits {
+  int32_t max_batch;           /* frames per run (default 1) */
+  int32_t max_net_h, max_net_w;/* largest network input, multiples of 8 (default 368 x 656) */
+  int32_t max_map_h, max_map_w;/* largest post-process map (default 320 x 576) */
+  int32_t max_peaks_per_joint; /* default 512 */
+  int32_t max_frame_h, max_frame_w; /* largest raw BGR frame for the staged path (default 720 x 1280) */
+} op_limits;
+
+/* Per-frame result header.  status is the frame's OP_* code. */
+typedef struct op_frame_result {
+  int32_t status;
+  int32_t n_peaks;   /* len(all_peaks) */
+  int32_t n_persons; /* len(subsets) after the keep filter (pose_detector.py:248) */
+  int32_t map_w, map_h;
+  int32_t net_w, net_h;
+} op_frame_result;
+
+typedef struct op_ctx op_ctx;
+
+const char* op_last_error(void);
+int op_default_params(op_params* p);
+int op_default_limits(op_limits* l);
+
+/* Layer table of models/CocoPoseNet.py:26-129 (name, Ci, Co, ksize) in declaration order. */
+int op_layer_info(int index, const char** name, int32_t* ci, int32_t* co, int32_t* ksize);
+
+/* PoseDetector.__init__ (pose_detector.py:16-35): context on HIP device `device`. */
+int op_create(const op_params* params, const op_limits* limits, int device, op_ctx** out);
+int op_destroy(op_ctx* ctx);
+
+/* serializers.load_npz(weights_file, model) (pose_detector.py:26): 92 layers in op_layer_info
+ * order, W as Chainer (Co, Ci, k, k) f32 and b as (Co,) f32.  Packed into the kernel layout
+ * and uploaded once. */
+int op_set_weights(op_ctx* ctx, const float* const* W, const float* const* b);
+
+/* PoseDetector.__call__ (pose_detector.py:484-517), single scale.  bgr: h x w x 3 uint8,
+ * row_stride bytes per row.  poses: cap x 18 x 3 f64, scores: cap f64. */
+int op_detect(op_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride,
+              double* poses, double* scores, int32_t cap, op_frame_result* res);
+
+/* ---- Stage entry points (same semantics as the named reference code; used by the parity tests) ---- */
+
+/* cv2.resize(orig_img, (out_w, out_h)) + preprocess (pose_detector.py:493-494, 426-431):
+ * x_out (1, 3, out_h, out_w) f32 = u8/255 - 0.5, BGR order kept. */
+int op_preprocess(op_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride,
+                  int32_t out_w, int32_t out_h, float* x_out);
+
+/* CocoPoseNet.__call__ (models/CocoPoseNet.py:132-262): x (n, 3, h, w) f32 -> last-stage
+ * pafs (n, 38, h/8, w/8) and heatmaps (n, 19, h/8, w/8).  h, w multiples of 8. */
+int op_forward(op_ctx* ctx, const float* x, int32_t n, int32_t h, int32_t w, float* pafs, float* heatmaps);
+
+/* F.resize_images (pose_detector.py:501-502; Chainer <= 6 align-corners bilinear): (c,h,w) -> (c,oh,ow). */
+int op_resize_images(op_ctx* ctx, const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y);
+
+/* compute_peaks_from_heatmaps (pose_detector.py:75-110, CPU semantics): heatmaps (c, h, w),
+ * channel c-1 dropped.  peaks: rows [joint, x, y, score, id] f64. */
+int op_compute_peaks(op_ctx* ctx, const float* heatmaps, int32_t c, int32_t h, int32_t w,
+                     double* peaks, int64_t cap, int64_t* n_peaks);
+
+/* compute_connections (pose_detector.py:161-181, with compute_candidate_connections :135-159):
+ * pafs (38, h, w) at map resolution, peaks (n, 5).  conn rows [id_a, id_b, score]; limb l's rows
+ * are conn[conn_off[l] .. conn_off[l+1]). */
+int op_compute_connections(op_ctx* ctx, const float* pafs, int32_t h, int32_t w, const double* peaks,
+                           int64_t n_peaks, double img_len, double* conn, int64_t cap, int64_t* conn_off);
+
+/* grouping_key_points (pose_detector.py:183-250): subsets (S, 20) f64 after the keep filter. */
+int op_grouping(op_ctx* ctx, const double* conn, const int64_t* conn_off, const double* peaks,
+                int64_t n_peaks, double* subsets, int64_t cap, int64_t* n_subsets);
+
+/* pose_detector.py:501-517 from the last-stage network maps (38,h,w) + (19,h,w) of one frame;
+ * the image was orig_h x orig_w. */
+int op_postprocess(op_ctx* ctx, const float* paf_low, const float* heat_low, int32_t h, int32_t w,
+                   int32_t orig_h, int32_t orig_w, double* poses, double* scores, int32_t cap,
+                   op_frame_result* res);
+
+/* ---- Device-resident batched path (frame-parallel serving / bench) ---- */
+
+/* Copy n BGR frames (n x h x w x 3 u8, contiguous) into the context's HBM staging area. */
+int op_stage_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, int32_t w);
+/* Optional: post-process these network-resolution maps (n x 57 x mh x mw: 38 PAF then 19 heat)
+ * instead of the network's own last stage (synthetic-map benchmarking; default off). */
+int op_stage_maps(op_ctx* ctx, const float* maps, int32_t n, int32_t mh, int32_t mw);
+int op_use_staged_maps(op_ctx* ctx, int32_t enable);
+/* Enqueue the full path (resize+normalise, 92 convs, post-process) on the staged frames; async. */
+int op_run_staged(op_ctx* ctx);
+/* Capture op_run_staged as a hipGraph and replay it (same semantics, fewer launches). */
+int op_run_staged_graph(op_ctx* ctx);
+int op_synchronize(op_ctx* ctx);
+/* Results of staged frame i (after op_synchronize). */
+int op_fetch_result(op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap, op_frame_result* res);
+
+/* HIP-event timing of the last op_run_staged: ms spent in the conv kernels, the post-process kernels
+ * and total, recorded on the context stream. */
+int op_last_timing(op_ctx* ctx, double* conv_ms, double* post_ms, double* total_ms);
+/* Per-kernel-class HIP-event timing of the launches enqueued by op_run_staged while enabled
+ * (event pairs on the context stream around every launch of the class).  Classes:
+ * 0 = 7x7 stage convs (the dominant kernel), 1 = 3x3 convs, 2 = 1x1 convs, 3 = post-process.
+ * op_profile_read resolves pending pairs (after op_synchronize) and returns the totals since the
+ * last reset: summed ms, launch count, algorithmic FLOPs and algorithmic HBM bytes. */
+int op_profile_enable(op_ctx* ctx, int32_t enable);
+int op_profile_read(op_ctx* ctx, int32_t cls, double* ms, int64_t* launches, double* flops, double* bytes);
+int op_profile_reset(op_ctx* ctx);
+
+/* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
+double op_forward_flops(int32_t h, int32_t w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPENPOSE_HIP_H */

@@ -178,6 +178,34 @@ def main():
         print("%-16s peaks=%4d conns=%4d persons=%s status=%d" % (
             name, len(ref["all_peaks"]), len(ref.get("conn", [])),
             ref["poses_shape"][0] if "poses_shape" in ref else "-", ref["status"]))
+    # grouping_key_points overflow: a connection that touches 3 subsets raises IndexError in the
+    # reference (pose_detector.py:197).  Search small random connection sets for one.
+    from entity import params as ref_params
+    found = None
+    for trial in range(20000):
+        npk = 12
+        peaks = np.zeros((npk, 5))
+        peaks[:, 0] = np.sort(rng.integers(0, 18, npk))
+        peaks[:, 1:3] = rng.integers(0, 40, (npk, 2))
+        peaks[:, 3] = rng.uniform(0.1, 1.0, npk)
+        peaks[:, 4] = np.arange(npk)
+        conns = []
+        for l, (ja, jb) in enumerate(ref_params["limbs_point"]):
+            ia = np.nonzero(peaks[:, 0] == ja)[0]
+            ib = np.nonzero(peaks[:, 0] == jb)[0]
+            rows = [[a, b, rng.uniform(0.1, 1.0)] for a in ia for b in ib if rng.uniform() < 0.7]
+            conns.append(np.array(rows, np.float64).reshape(-1, 3))
+        try:
+            pd.grouping_key_points(conns, peaks, ref_params)
+        except IndexError:
+            found = (peaks, conns)
+            break
+    assert found is not None
+    peaks, conns = found
+    np.savez_compressed(os.path.join(HERE, "grouping_indexerror.npz"), all_peaks=peaks,
+                        conn=np.concatenate(conns), conn_off=np.concatenate([[0], np.cumsum([len(c) for c in conns])]),
+                        status=4, grouping_only=1)
+    print("grouping_indexerror found at trial", trial)
     # SciPy's own gaussian_filter on one upsampled map (pins the Gaussian restatement alone)
     from scipy.ndimage import gaussian_filter
     from oracle import postproc

@@ -1,0 +1,50 @@
+"""The C-ABI library loads and exports every declared symbol (no compute: no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def _declared():
+    src = open(os.path.join(REPO, "include", "openpose_hip.h")).read()
+    return sorted(set(re.findall(r"\b(op_[a-z_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported(lib):
+    L = ctypes.CDLL(lib.LIB_PATH)
+    decl = _declared()
+    assert len(decl) >= 20
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(lib.EXPORTED) == decl
+
+
+def test_layer_table_matches_cocoposenet(lib):
+    from oracle.forward import LAYERS
+    assert lib.layer_table() == LAYERS
+
+
+def test_forward_flops(lib):
+    # 271.9 GFLOP per 368x368 frame, 484.6 at 656x368
+    assert abs(lib.forward_flops(368, 368) / 1e9 - 271.868) < 0.01
+    assert abs(lib.forward_flops(368, 656) / 1e9 - 484.6) < 0.1
+
+
+def test_default_params_mirror_entity(lib, pkg):
+    p = lib.default_params()
+    prm = pkg.params
+    assert p.inference_img_size == prm["inference_img_size"] and p.heatmap_size == prm["heatmap_size"]
+    assert p.gaussian_sigma == prm["gaussian_sigma"] and p.n_integ_points == prm["n_integ_points"]
+    assert [[p.limbs_point[i][0], p.limbs_point[i][1]] for i in range(19)] == [[int(a), int(b)] for a, b in prm["limbs_point"]]
+
+
+def test_no_silent_cpu_path(lib):
+    """Without a GPU the product path must fail loudly, never fall back."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        lib.Context(0)

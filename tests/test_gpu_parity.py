@@ -1,0 +1,140 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and the reference goldens.
+
+Bit-exact for the integer/index work and the post-process (which restates f64/f32 NumPy/SciPy
+arithmetic exactly); the fp32 forward is held to |gpu - oracle| <= 1e-3 (north star) on maps
+of O(1) magnitude."""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden, people_image, pkg_module
+from oracle import cvresize, postproc as P
+from oracle import forward as F
+
+pytestmark = pytest.mark.gpu
+FWD_TOL = 1e-3
+
+
+@pytest.mark.parametrize("shape", [(584, 584), (480, 640), (642, 482), (37, 53), (720, 1280)])
+def test_preprocess_bit_exact(ctx, shape):
+    rng = np.random.default_rng(shape[0])
+    img = rng.integers(0, 256, shape + (3,), dtype=np.uint8)
+    w, h = cvresize.compute_optimal_size(shape[0], shape[1], 368)
+    got = ctx.preprocess(img, w, h)
+    want = cvresize.preprocess(cvresize.resize_linear_u8(img, w, h))
+    assert np.array_equal(got, want)
+
+
+def test_preprocess_people_png(ctx):
+    img = people_image()
+    got = ctx.preprocess(img, 368, 368)
+    assert np.array_equal(got, cvresize.preprocess(cvresize.resize_linear_u8(img, 368, 368)))
+
+
+@pytest.mark.parametrize("src,dst", [((46, 46), (320, 320)), ((46, 82), (320, 576)), ((62, 46), (432, 320)),
+                                     ((5, 7), (40, 13))])
+def test_resize_images_bit_exact(ctx, src, dst):
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((5,) + src).astype(np.float32)
+    assert np.array_equal(ctx.resize_images(x, *dst), P.resize_images(x, *dst))
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_peaks_connections_grouping_vs_reference(ctx, case):
+    d = load_golden(case)
+    mh, mw = int(d["map_h"]), int(d["map_w"])
+    heat = P.resize_images(d["heat_low"], mh, mw)
+    peaks = ctx.compute_peaks(heat)
+    assert np.array_equal(peaks.reshape(-1, 5), d["all_peaks"])
+    if int(d["status"]) == 1:
+        return
+    pafs = P.resize_images(d["paf_low"], mh, mw)
+    conns = ctx.compute_connections(pafs, peaks, mw)
+    assert np.array_equal(np.concatenate(conns), d["conn"])
+    subsets = ctx.grouping(conns, peaks)
+    assert np.array_equal(subsets, d["subsets"])
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_postprocess_from_network_maps_vs_reference(ctx, case):
+    d = load_golden(case)
+    poses, scores, res = ctx.postprocess(d["paf_low"], d["heat_low"], int(d["orig_h"]), int(d["orig_w"]))
+    assert res.n_peaks == len(d["all_peaks"])
+    if int(d["status"]) == 1:
+        assert res.n_persons == 0
+        return
+    assert res.n_persons == int(d["poses_shape"][0])
+    assert np.array_equal(poses.reshape(d["poses"].shape), d["poses"])
+    assert np.array_equal(scores, d["scores"])
+
+
+def test_grouping_indexerror(ctx):
+    d = load_golden("grouping_indexerror")
+    off = d["conn_off"]
+    with pytest.raises(IndexError):
+        ctx.grouping([d["conn"][off[l]:off[l + 1]] for l in range(19)], d["all_peaks"])
+
+
+def _fwd_check(ctx, weights, x):
+    paf, heat = ctx.forward(x)
+    opaf, oheat = F.cocoposenet_forward(weights, x)
+    err = max(float(np.abs(paf - opaf).max()), float(np.abs(heat - oheat).max()))
+    mag = max(float(np.abs(opaf).max()), float(np.abs(oheat).max()))
+    print("forward %s: max|gpu-oracle| = %.3g (max|map| = %.3g)" % (x.shape, err, mag))
+    assert err <= FWD_TOL
+    return paf, heat
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 64, 80), (2, 3, 48, 48)])
+def test_forward_small_vs_oracle(ctx, rand_weights, shape):
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-0.5, 0.5, shape).astype(np.float32)
+    _fwd_check(ctx, rand_weights, x)
+
+
+def test_forward_368_vs_oracle(ctx, rand_weights):
+    x = cvresize.preprocess(cvresize.resize_linear_u8(people_image(), 368, 368))
+    _fwd_check(ctx, rand_weights, x)
+
+
+def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
+    """PoseDetector(img) == oracle post-process of the GPU forward of the GPU-preprocessed image."""
+    det = pkg.PoseDetector("posenet", model=rand_weights, device=0)
+    img = people_image()
+    x = det._ctx.preprocess(img, 368, 368)
+    paf, heat = det._ctx.forward(x)
+    want_p, want_s = P.postprocess(paf[0], heat[0], img.shape[0], img.shape[1])
+    poses, scores = det(img)
+    assert np.asarray(poses).shape == np.asarray(want_p).shape
+    assert np.array_equal(np.asarray(poses, np.float64), np.asarray(want_p, np.float64))
+    assert np.array_equal(scores, want_s)
+
+
+def test_staged_batch_matches_single_and_graph(ctx):
+    rng = np.random.default_rng(3)
+    frames = rng.integers(0, 256, (3, 300, 420, 3), dtype=np.uint8)
+    single = [ctx.detect(f) for f in frames]
+    ctx.stage_frames(frames)
+    for graph in (False, True, True):
+        ctx.run_staged(graph=graph)
+        ctx.synchronize()
+        for i in range(3):
+            p, s, r = ctx.fetch_result(i)
+            assert r.n_peaks == single[i][2].n_peaks
+            assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
+
+
+def test_staged_synthetic_maps_match_reference(ctx):
+    d = load_golden("six_people")
+    maps = np.concatenate([d["paf_low"], d["heat_low"]])[None].repeat(2, axis=0)
+    frames = np.zeros((2, int(d["orig_h"]), int(d["orig_w"]), 3), np.uint8)
+    ctx.stage_frames(frames)
+    ctx.stage_maps(maps)
+    ctx.use_staged_maps(True)
+    try:
+        ctx.run_staged()
+        ctx.synchronize()
+        for i in range(2):
+            p, s, r = ctx.fetch_result(i)
+            assert np.array_equal(p.reshape(d["poses"].shape), d["poses"]) and np.array_equal(s, d["scores"])
+    finally:
+        ctx.use_staged_maps(False)
