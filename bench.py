@@ -21,6 +21,7 @@ sys.path.insert(0, REPO)
 PKG = "chainer_realtime_multi-person_pose_estimation_amd"
 METRIC = "frames/sec end-to-end (CNN+PAF grouping) at 368×368, 1/2/4/8 MI355X"
 FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA peak
 HBM_PEAK_GBS = 8000.0
 
 
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--precision", choices=["bf16x3", "fp32"], default="bf16x3",
+                    help="conv arithmetic: 3xBF16-split products (f32 accumulate) or exact f32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,6 +92,7 @@ def main():
     limits = L.OpLimits()
     limits.max_batch = B
     ctx = L.Context(local, None, limits)
+    ctx.set_precision(args.precision)
     ctx.set_weights(Wm.random_weights(seed=0))
     rng = np.random.default_rng(1234 + rank)
     frames = rng.integers(0, 256, (B, 368, 368, 3), dtype=np.uint8)
@@ -148,16 +152,24 @@ def main():
     roofline = None
     if n7 > 0 and ms7 > 0:
         achieved = fl7 / (ms7 * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "conv_mfma_f32<7,2,2> (7x7 stage convs)",
-                    "achieved": round(achieved, 2), "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_MATRIX_PEAK_TFLOPS, 4), "traffic": None,
+        if args.precision == "bf16x3":
+            # 3 bf16 MFMA products per f32-accurate MAC: the f32-accurate peak is 2500/3 TFLOP/s
+            peak = BF16_DENSE_PEAK_TFLOPS / 3.0
+            kern = "conv_bf16x3<7,4,2> (7x7 stage convs, 3xBF16 split on v_mfma_f32_32x32x16_bf16)"
+        else:
+            peak = FP32_MATRIX_PEAK_TFLOPS
+            kern = "conv_mfma_f32<7,2,2> (7x7 stage convs, v_mfma_f32_32x32x2_f32)"
+        roofline = {"bound": "mfma", "kernel": kern,
+                    "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": None,
                     "launch_ms": round(ms7 / n7, 4), "flops_per_launch": fl7 / n7,
                     "algorithmic_bytes_per_launch": by7 / n7}
     stage_ms = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16x3 (hi/lo split operands, f32 accumulate)" if args.precision == "bf16x3" else "f32",
         "data": "synthetic: seeded uint8 368x368 BGR frames resident in HBM; random-init CocoPoseNet (He-normal); "
                 + ("post-process fed COCO-like 6-person network maps (reference label generators)"
                    if args.maps == "synthetic" else "post-process fed the network's own last stage"),

@@ -22,7 +22,9 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
+    "op_set_precision", "op_get_precision",
 )
+PRECISION = {"fp32": 0, "bf16x3": 1}
 
 
 class OpParams(ctypes.Structure):
@@ -89,6 +91,8 @@ def lib():
         "op_profile_enable": ([P, I32], ctypes.c_int),
         "op_profile_read": ([P, I32, P, P, P, P], ctypes.c_int),
         "op_profile_reset": ([P], ctypes.c_int),
+        "op_set_precision": ([P, I32], ctypes.c_int),
+        "op_get_precision": ([P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -177,6 +181,15 @@ class Context(object):
             self.close()
         except Exception:
             pass
+
+    def set_precision(self, mode):
+        """'bf16x3' (default: 3xBF16 split products, f32 accumulate) or 'fp32' (exact f32 MFMA)."""
+        check(lib().op_set_precision(self.h, PRECISION[mode]), "op_set_precision")
+
+    def get_precision(self):
+        m = ctypes.c_int32()
+        check(lib().op_get_precision(self.h, ctypes.byref(m)), "op_get_precision")
+        return {v: k for k, v in PRECISION.items()}[m.value]
 
     def set_weights(self, weights):
         """weights: {layer name: (W (Co,Ci,k,k) f32, b (Co,) f32)}."""

@@ -29,7 +29,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int kCatStride = 192;
 constexpr int kCatFeat = 0;    // 128 channels
 constexpr int kCatHeat = 128;  // 19 channels (+1 zero pad)
-constexpr int kCatPaf = 148;   // 38 channels (+2 zero pad)
+constexpr int kCatPaf = 152;   // 38 channels (+2 zero pad); 8-channel aligned for the split format
 constexpr int kStagePad = 3;   // halo of the 7x7 stage convs
 
 // ---- launch helpers implemented in the .hip files ----
@@ -53,6 +53,28 @@ struct ConvShape {
 };
 
 int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st);
+
+// ---- 3xBF16 split path (conv_bf16x3.hip) ----
+struct SplitConvGroup {
+  const float* in;      // split NHWC input, offset by the group's first input channel (multiple of 16)
+  float* out;           // split NHWC output, offset by the group's first output channel (multiple of 8)
+  const void* w;        // packed [c16][tap][cop][k-half][hi8 lo8] bf16
+  const float* bias;    // [cop] f32
+  int32_t cop, cout_store, cin_off;
+  float* out32;         // optional dense f32 copy of the output (n*h*w, cs_out32), or null
+  int32_t out32_off;
+};
+struct SplitConvShape {
+  int32_t n, h, w, pin, cs_in, pout, cs_out, c16, ks, relu, groups, cs_out32;
+};
+int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st);
+int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
+                          int32_t c, hipStream_t st);
+int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);
+int launch_preprocess_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t n, int32_t sh,
+                            int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st);
+int launch_extract_maps32(const float* m, int32_t cs, int32_t heat_off, int32_t n, int32_t h, int32_t w, float* paf,
+                          float* heat, hipStream_t st);
 int launch_maxpool2(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
                     int32_t c, hipStream_t st);
 int launch_nchw_to_nhwc8(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);

@@ -75,6 +75,8 @@ struct PackedConv {
   float* b = nullptr;
   int cop = 0, cin_phys = 0, ks = 0;
   int cin_log = 0, co_log = 0;  // logical (reference) channel counts, for algorithmic FLOPs
+  void* ws = nullptr;           // 3xBF16 split weights [c16][tap][cop][k-half][hi8 lo8]
+  int cin16 = 0;                // input channels padded to 16 (split path)
 };
 
 struct ProfPair {
@@ -112,11 +114,54 @@ static void pack_into(std::vector<float>& dst, std::vector<float>& bias, int cop
   (void)c8;
 }
 
+static inline uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);  // inf / nan: truncate
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static inline float bf16_f(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// Pack Chainer W (Co, Ci, k, k) into the split layout at output-channel offset co_off:
+// element (c16, tap, co, h, part, j) = part 0: bf16(w), part 1: bf16(w - hi) for input channel 16*c16 + 8h + j.
+static void pack_split_into(std::vector<uint16_t>& dst, int cop, int cin16, int k, const float* W, int Co, int Ci,
+                            int co_off, bool cat_input) {
+  const int taps = k * k;
+  for (int co = 0; co < Co; ++co)
+    for (int p = 0; p < cin16; ++p) {
+      const int ci = cat_input ? cat_logical(p) : (p < Ci ? p : -1);
+      if (ci < 0) continue;
+      const int c16 = p / 16, h = (p % 16) / 8, j = p % 8;
+      for (int t = 0; t < taps; ++t) {
+        const int ky = t / k, kx = t % k;
+        const float v = W[(((size_t)co * Ci + ci) * k + ky) * k + kx];
+        const uint16_t hb = bf16_rne(v);
+        const uint16_t lb = bf16_rne(v - bf16_f(hb));
+        const size_t base = ((((size_t)c16 * taps + t) * cop + (co_off + co)) * 2 + h) * 16;
+        dst[base + j] = hb;
+        dst[base + 8 + j] = lb;
+      }
+    }
+}
+
 static int upload(PackedConv& pc, const std::vector<float>& w, const std::vector<float>& b) {
   OP_HIP_CHECK(hipMalloc(&pc.w, w.size() * sizeof(float)));
   OP_HIP_CHECK(hipMalloc(&pc.b, b.size() * sizeof(float)));
   OP_HIP_CHECK(hipMemcpy(pc.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
   OP_HIP_CHECK(hipMemcpy(pc.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+  return OP_OK;
+}
+
+static int upload_split(PackedConv& pc, const std::vector<uint16_t>& ws) {
+  OP_HIP_CHECK(hipMalloc(&pc.ws, ws.size() * sizeof(uint16_t)));
+  OP_HIP_CHECK(hipMemcpy(pc.ws, ws.data(), ws.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   return OP_OK;
 }
 
@@ -131,7 +176,7 @@ struct Act {
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
-  B_S1, B_COUNT
+  B_S1, B_MAP32, B_COUNT
 };
 
 }  // namespace op
@@ -156,6 +201,8 @@ struct op_ctx {
   void* arena = nullptr;
   size_t arena_bytes = 0;
   int gn = 0, gh = 0, gw = 0;  // current geometry (batch, net h, net w)
+  bool split = true;           // 3xBF16 split convs (default) or exact f32 MFMA convs
+  bool gsplit = true;          // format the arena is currently carved for
   Act buf[B_COUNT];
   // post-process
   PostBuffers pb{};
@@ -192,7 +239,7 @@ struct op_ctx {
 
 namespace op {
 
-static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out) {
+static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) {
   // (pad, channel stride, scale divisor) per buffer
   struct D {
     int pad, cs, div;
@@ -200,12 +247,12 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out) {
   const D d[B_COUNT] = {{1, 8, 1},   {1, 64, 1},  {0, 64, 1},  {1, 64, 2},  {1, 128, 2}, {0, 128, 2},
                         {1, 128, 4}, {1, 256, 4}, {1, 256, 4}, {0, 256, 4}, {1, 256, 8}, {1, 512, 8},
                         {1, 512, 8}, {1, 256, 8}, {kStagePad, kCatStride, 8}, {kStagePad, 256, 8},
-                        {kStagePad, 256, 8}, {0, 1024, 8}};
+                        {kStagePad, 256, 8}, {0, 1024, 8}, {0, 64, 8}};
   size_t total = 0;
   for (int i = 0; i < B_COUNT; ++i) {
     Act a;
     a.pad = d[i].pad;
-    a.cs = d[i].cs;
+    a.cs = (i == B_X0 && split) ? 16 : d[i].cs;
     a.h = h / d[i].div;
     a.w = w / d[i].div;
     const size_t fl = a.frame_floats() * (size_t)n;
@@ -224,9 +271,9 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
     set_error("network input must be >= 16 and a multiple of 8");
     return OP_ERR_INVALID;
   }
-  if (c->gn == n && c->gh == h && c->gw == w) return OP_OK;
+  if (c->gn == n && c->gh == h && c->gw == w && c->gsplit == c->split) return OP_OK;
   Act a[B_COUNT];
-  const size_t need = geom_floats(c, n, h, w, a) * sizeof(float);
+  const size_t need = geom_floats(c, n, h, w, a, c->split) * sizeof(float);
   if (need > c->arena_bytes) {
     if (c->arena) OP_HIP_CHECK(hipFree(c->arena));
     c->arena = nullptr;
@@ -245,6 +292,7 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   c->gn = n;
   c->gh = h;
   c->gw = w;
+  c->gsplit = c->split;
   return OP_OK;
 }
 
@@ -376,8 +424,50 @@ static void conv_work(const op_ctx* c, const Act& out, const PackedConv& pc, dou
   *bytes += 4.0 * (px * pc.cin_log + px * pc.co_log + (double)pc.cin_log * pc.co_log * pc.ks * pc.ks + pc.co_log);
 }
 
+static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_off, const PackedConv& pc,
+                          int cout_store) {
+  SplitConvGroup g;
+  g.in = in.p + cin_off;
+  g.out = out.p + cout_off;
+  g.w = pc.ws;
+  g.bias = pc.b;
+  g.cop = pc.cop;
+  g.cout_store = cout_store;
+  g.cin_off = cin_off;
+  g.out32 = nullptr;
+  g.out32_off = 0;
+  return g;
+}
+
+static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups) {
+  SplitConvShape s;
+  s.n = n;
+  s.h = out.h;
+  s.w = out.w;
+  s.pin = in.pad;
+  s.cs_in = in.cs;
+  s.pout = out.pad;
+  s.cs_out = out.cs;
+  s.c16 = c16;
+  s.ks = ks;
+  s.relu = relu ? 1 : 0;
+  s.groups = groups;
+  s.cs_out32 = 0;
+  return s;
+}
+
 static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout_off, const PackedConv& pc, int store,
                  bool relu) {
+  if (c->split) {
+    SplitConvGroup g[2];
+    g[0] = sgrp(in, cin_off, out, cout_off, pc, store);
+    g[1] = g[0];
+    double fl = 0, by = 0;
+    conv_work(c, out, pc, &fl, &by);
+    return profiled(c, conv_class(pc.ks), fl, by, [&] {
+      return launch_conv_bf16x3(sshp(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, 1), g, c->stream);
+    });
+  }
   ConvGroup g[2];
   g[0] = grp(in, cin_off, out, cout_off, pc, store);
   g[1] = g[0];
@@ -388,7 +478,24 @@ static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout
 }
 
 static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1, const PackedConv& p0,
-                 const PackedConv& p1, int st0, int st1, bool relu) {
+                 const PackedConv& p1, int st0, int st1, bool relu, const Act* out32 = nullptr, int o32a = 0,
+                 int o32b = 0) {
+  if (c->split) {
+    SplitConvGroup g[2];
+    g[0] = sgrp(in, ci0, out, co0, p0, st0);
+    g[1] = sgrp(in, ci1, out, co1, p1, st1);
+    SplitConvShape sh = sshp(c->gn, in, out, p0.cin16 / 16, p0.ks, relu, 2);
+    if (out32) {
+      g[0].out32 = g[1].out32 = out32->p;
+      g[0].out32_off = o32a;
+      g[1].out32_off = o32b;
+      sh.cs_out32 = out32->cs;
+    }
+    double fl = 0, by = 0;
+    conv_work(c, out, p0, &fl, &by);
+    conv_work(c, out, p1, &fl, &by);
+    return profiled(c, conv_class(p0.ks), fl, by, [&] { return launch_conv_bf16x3(sh, g, c->stream); });
+  }
   ConvGroup g[2];
   g[0] = grp(in, ci0, out, co0, p0, st0);
   g[1] = grp(in, ci1, out, co1, p1, st1);
@@ -405,19 +512,24 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
     if (_r) return _r;   \
   } while (0)
 
+static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
+  if (c->split) return launch_maxpool2_split(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
+  return launch_maxpool2(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
+}
+
 static int run_forward(op_ctx* c) {
   Act* B = c->buf;
   RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
   RC(conv1(c, B[B_C11], 0, B[B_C12], 0, c->bb[1], 64, true));
-  RC(launch_maxpool2(B[B_C12].p, 0, B[B_P1].p, 1, c->gn, B[B_C12].h, B[B_C12].w, 64, c->stream));
+  RC(pool(c, B[B_C12], B[B_P1], 64));
   RC(conv1(c, B[B_P1], 0, B[B_C21], 0, c->bb[2], 128, true));
   RC(conv1(c, B[B_C21], 0, B[B_C22], 0, c->bb[3], 128, true));
-  RC(launch_maxpool2(B[B_C22].p, 0, B[B_P2].p, 1, c->gn, B[B_C22].h, B[B_C22].w, 128, c->stream));
+  RC(pool(c, B[B_C22], B[B_P2], 128));
   RC(conv1(c, B[B_P2], 0, B[B_C3A], 0, c->bb[4], 256, true));
   RC(conv1(c, B[B_C3A], 0, B[B_C3B], 0, c->bb[5], 256, true));
   RC(conv1(c, B[B_C3B], 0, B[B_C3A], 0, c->bb[6], 256, true));
   RC(conv1(c, B[B_C3A], 0, B[B_C34], 0, c->bb[7], 256, true));
-  RC(launch_maxpool2(B[B_C34].p, 0, B[B_P3].p, 1, c->gn, B[B_C34].h, B[B_C34].w, 256, c->stream));
+  RC(pool(c, B[B_C34], B[B_P3], 256));
   RC(conv1(c, B[B_P3], 0, B[B_C41], 0, c->bb[8], 512, true));
   RC(conv1(c, B[B_C41], 0, B[B_C42], 0, c->bb[9], 512, true));
   RC(conv1(c, B[B_C42], 0, B[B_C43], 0, c->bb[10], 256, true));
@@ -442,7 +554,9 @@ static int run_forward(op_ctx* c) {
       std::swap(src, dst);
     }
     RC(conv2(c, *src, 0, 128, s6, 0, 128, c->st_g[st][0][4], c->st_g[st][1][4], 128, 128, true));
-    RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false));
+    // the last stage also leaves a dense f32 copy (paf at 0, heat at 40) for the post-process
+    RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false,
+             (c->split && st == 4) ? &B[B_MAP32] : nullptr, 0, 40));
   }
   return OP_OK;
 }
@@ -662,7 +776,9 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
 static void free_pc(op::PackedConv& p) {
   if (p.w) hipFree(p.w);
   if (p.b) hipFree(p.b);
+  if (p.ws) hipFree(p.ws);
   p.w = p.b = nullptr;
+  p.ws = nullptr;
 }
 
 static void free_weights(op_ctx* c) {
@@ -722,8 +838,12 @@ int op_set_weights(op_ctx* c, const float* const* W, const float* const* b) {
     pc.cop = round_up(d.co, 64);
     pc.cin_log = d.ci;
     pc.co_log = d.co;
+    pc.cin16 = cat_in ? kCatStride : round_up(d.ci, 16);
     std::vector<float> w((size_t)pc.cin_phys * d.k * d.k * pc.cop, 0.0f), bias(pc.cop, 0.0f);
     pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[li], b[li], d.co, d.ci, 0, cat_in);
+    std::vector<uint16_t> ws((size_t)pc.cin16 * d.k * d.k * pc.cop * 2, 0);
+    pack_split_into(ws, pc.cop, pc.cin16, d.k, W[li], d.co, d.ci, 0, cat_in);
+    RC(upload_split(pc, ws));
     return upload(pc, w, bias);
   };
   auto fused = [&](PackedConv& pc, int l1, int l2, bool cat_in) -> int {
@@ -733,9 +853,14 @@ int op_set_weights(op_ctx* c, const float* const* W, const float* const* b) {
     pc.cop = 2 * d.co;
     pc.cin_log = d.ci;
     pc.co_log = 2 * d.co;
+    pc.cin16 = cat_in ? kCatStride : round_up(d.ci, 16);
     std::vector<float> w((size_t)pc.cin_phys * d.k * d.k * pc.cop, 0.0f), bias(pc.cop, 0.0f);
     pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[l1], b[l1], d.co, d.ci, 0, cat_in);
     pack_into(w, bias, pc.cop, pc.cin_phys, d.k, W[l2], b[l2], d.co, d.ci, d.co, cat_in);
+    std::vector<uint16_t> ws((size_t)pc.cin16 * d.k * d.k * pc.cop * 2, 0);
+    pack_split_into(ws, pc.cop, pc.cin16, d.k, W[l1], d.co, d.ci, 0, cat_in);
+    pack_split_into(ws, pc.cop, pc.cin16, d.k, W[l2], d.co, d.ci, d.co, cat_in);
+    RC(upload_split(pc, ws));
     return upload(pc, w, bias);
   };
   for (int i = 0; i < 12; ++i) RC(single(c->bb[i], i, false));
@@ -793,11 +918,17 @@ int op_forward(op_ctx* c, const float* x, int32_t n, int32_t h, int32_t w, float
   float* dx = c->d_scratch;
   float* dmaps = (float*)((char*)c->d_scratch + (xin + 255) / 256 * 256);
   OP_HIP_CHECK(hipMemcpyAsync(dx, x, xin, hipMemcpyHostToDevice, c->stream));
-  RC(launch_nchw_to_nhwc8(dx, c->buf[B_X0].p, n, h, w, c->stream));
+  if (c->split)
+    RC(launch_nchw_to_split16(dx, c->buf[B_X0].p, n, h, w, c->stream));
+  else
+    RC(launch_nchw_to_nhwc8(dx, c->buf[B_X0].p, n, h, w, c->stream));
   RC(run_forward(c));
   float* dpaf = dmaps;
   float* dheat = dmaps + (size_t)n * 38 * lh * lw;
-  RC(launch_extract_maps(c->buf[B_CAT].p, n, lh, lw, dpaf, dheat, c->stream));
+  if (c->split)
+    RC(launch_extract_maps32(c->buf[B_MAP32].p, 64, 40, n, lh, lw, dpaf, dheat, c->stream));
+  else
+    RC(launch_extract_maps(c->buf[B_CAT].p, n, lh, lw, dpaf, dheat, c->stream));
   OP_HIP_CHECK(hipMemcpyAsync(pafs, dpaf, (size_t)n * 38 * lh * lw * 4, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipMemcpyAsync(heatmaps, dheat, (size_t)n * 19 * lh * lw * 4, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -1073,8 +1204,12 @@ static int enqueue_staged(op_ctx* c, bool timing) {
   RC(ensure_geometry(c, c->st_n, in_h, in_w));
   RC(ensure_post(c, c->st_n, map_h, map_w));
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[0], c->stream));
-  RC(launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h, c->st_w,
-                       in_h, in_w, c->buf[B_X0].p, c->stream));
+  if (c->split)
+    RC(launch_preprocess_split(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h,
+                               c->st_w, in_h, in_w, c->buf[B_X0].p, c->stream));
+  else
+    RC(launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h, c->st_w,
+                         in_h, in_w, c->buf[B_X0].p, c->stream));
   RC(run_forward(c));
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[1], c->stream));
   const int lh = in_h / 8, lw = in_w / 8;
@@ -1085,6 +1220,9 @@ static int enqueue_staged(op_ctx* c, bool timing) {
       return OP_ERR_STATE;
     }
     src = MapSource{c->d_maps, (int64_t)57 * lh * lw, 0, 57, 0, 38};
+  } else if (c->split) {
+    const Act& m = c->buf[B_MAP32];
+    src = MapSource{m.p, (int64_t)m.frame_floats(), 0, m.cs, 0, 40};
   } else {
     const Act& cat = c->buf[B_CAT];
     src = MapSource{cat.p, (int64_t)cat.frame_floats(), cat.pad, cat.cs, kCatPaf, kCatHeat};
@@ -1185,7 +1323,7 @@ int op_run_staged_graph(op_ctx* c) {
   // the graph bakes in every pointer and size: replay only if none changed since capture
   const uintptr_t key[10] = {(uintptr_t)c->st_n, (uintptr_t)c->st_h, (uintptr_t)c->st_w, (uintptr_t)c->use_maps,
                              (uintptr_t)c->arena, (uintptr_t)c->post_arena, (uintptr_t)c->d_frames,
-                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw)};
+                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw) * 2 + (uintptr_t)c->split};
   if (c->gexec && memcmp(key, c->g_key, sizeof(key)) != 0) {
     hipGraphExecDestroy(c->gexec);
     c->gexec = nullptr;
@@ -1270,6 +1408,24 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
   if (rc) return rc;
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   return op_fetch_result(c, 0, poses, scores, cap, res);
+}
+
+int op_set_precision(op_ctx* c, int32_t mode) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (mode != OP_PRECISION_FP32 && mode != OP_PRECISION_BF16X3) {
+    set_error("precision must be OP_PRECISION_FP32 or OP_PRECISION_BF16X3");
+    return OP_ERR_INVALID;
+  }
+  c->split = mode == OP_PRECISION_BF16X3;
+  return OP_OK;
+}
+
+int op_get_precision(op_ctx* c, int32_t* mode) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (mode) *mode = c->split ? OP_PRECISION_BF16X3 : OP_PRECISION_FP32;
+  return OP_OK;
 }
 
 int op_profile_enable(op_ctx* c, int32_t enable) {

@@ -24,9 +24,12 @@ class PoseDetector(object):
            reference's ``model=`` it skips loading from disk.
     device: HIP device ordinal (negative -> 0).
     precise: multi-scale inference (pose_detector.py:433-482).
+    precision: 'bf16x3' (default; 3xBF16-split products with f32 accumulation, |err| ~3e-5 on the
+               maps) or 'fp32' (exact f32 products on the f32 matrix cores).
     """
 
-    def __init__(self, arch=None, weights_file=None, model=None, device=-1, precise=False, max_batch=1):
+    def __init__(self, arch=None, weights_file=None, model=None, device=-1, precise=False, max_batch=1,
+                 precision="bf16x3"):
         self.arch = arch
         self.precise = precise
         if model is None and arch not in (None, "posenet"):
@@ -35,6 +38,7 @@ class PoseDetector(object):
         limits = _lib.OpLimits()
         limits.max_batch = int(max_batch)
         self._ctx = _lib.Context(self.device, _lib.params_from_dict(params), limits)
+        self._ctx.set_precision(precision)
         if model is not None:
             w = model
         elif weights_file:

@@ -82,6 +82,15 @@ int op_layer_info(int index, const char** name, int32_t* ci, int32_t* co, int32_
 int op_create(const op_params* params, const op_limits* limits, int device, op_ctx** out);
 int op_destroy(op_ctx* ctx);
 
+/* Arithmetic of the forward convolutions.  OP_PRECISION_BF16X3 (default): every f32 operand is
+ * split into bf16 hi + lo and each product formed as hi*hi + hi*lo + lo*hi on the bf16 matrix
+ * cores with f32 accumulation (~16-bit products, 5.3x the f32-MFMA rate; |err| ~3e-5 on the maps,
+ * inside the 1e-3 parity tolerance).  OP_PRECISION_FP32: exact f32 products (v_mfma_f32_32x32x2_f32). */
+#define OP_PRECISION_FP32 0
+#define OP_PRECISION_BF16X3 1
+int op_set_precision(op_ctx* ctx, int32_t mode);
+int op_get_precision(op_ctx* ctx, int32_t* mode);
+
 /* serializers.load_npz(weights_file, model) (pose_detector.py:26): 92 layers in op_layer_info
  * order, W as Chainer (Co, Ci, k, k) f32 and b as (Co,) f32.  Packed into the kernel layout
  * and uploaded once. */

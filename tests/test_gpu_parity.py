@@ -84,16 +84,36 @@ def _fwd_check(ctx, weights, x):
     return paf, heat
 
 
-@pytest.mark.parametrize("shape", [(1, 3, 64, 80), (2, 3, 48, 48)])
-def test_forward_small_vs_oracle(ctx, rand_weights, shape):
+@pytest.fixture(params=["bf16x3", "fp32"])
+def precision_ctx(request, ctx):
+    ctx.set_precision(request.param)
+    yield ctx
+    ctx.set_precision("bf16x3")
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 64, 80), (2, 3, 48, 48), (3, 3, 40, 56)])
+def test_forward_small_vs_oracle(precision_ctx, rand_weights, shape):
     rng = np.random.default_rng(11)
     x = rng.uniform(-0.5, 0.5, shape).astype(np.float32)
-    _fwd_check(ctx, rand_weights, x)
+    _fwd_check(precision_ctx, rand_weights, x)
 
 
-def test_forward_368_vs_oracle(ctx, rand_weights):
+def test_forward_368_vs_oracle(precision_ctx, rand_weights):
     x = cvresize.preprocess(cvresize.resize_linear_u8(people_image(), 368, 368))
-    _fwd_check(ctx, rand_weights, x)
+    _fwd_check(precision_ctx, rand_weights, x)
+
+
+def test_forward_precisions_agree(ctx, rand_weights):
+    """bf16x3 vs exact-f32 MFMA on a 720p-shaped input (656x368), batch 2."""
+    rng = np.random.default_rng(2)
+    x = rng.uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
+    ctx.set_precision("fp32")
+    p32, h32 = ctx.forward(x)
+    ctx.set_precision("bf16x3")
+    p16, h16 = ctx.forward(x)
+    err = max(float(np.abs(p32 - p16).max()), float(np.abs(h32 - h16).max()))
+    print("bf16x3 vs fp32 at 656x368: %.3g" % err)
+    assert err <= FWD_TOL
 
 
 def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
@@ -109,7 +129,9 @@ def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
     assert np.array_equal(scores, want_s)
 
 
-def test_staged_batch_matches_single_and_graph(ctx):
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+def test_staged_batch_matches_single_and_graph(ctx, prec):
+    ctx.set_precision(prec)
     rng = np.random.default_rng(3)
     frames = rng.integers(0, 256, (3, 300, 420, 3), dtype=np.uint8)
     single = [ctx.detect(f) for f in frames]
@@ -121,6 +143,7 @@ def test_staged_batch_matches_single_and_graph(ctx):
             p, s, r = ctx.fetch_result(i)
             assert r.n_peaks == single[i][2].n_peaks
             assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
+    ctx.set_precision("bf16x3")
 
 
 def test_staged_synthetic_maps_match_reference(ctx):
