@@ -1,0 +1,8 @@
+"""Drop-in shim: the reference's callers do ``from pose_detector import PoseDetector``
+(pose_detector.py:15); this re-exports the MI355X implementation."""
+import importlib as _il
+
+_pkg = _il.import_module("chainer_realtime_multi-person_pose_estimation_amd")
+PoseDetector = _pkg.PoseDetector
+params = _pkg.params
+JointType = _pkg.JointType
