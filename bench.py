@@ -63,7 +63,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=28,
+                    help="frames per step per GPU (28 fills 2 workgroups/CU of the 7x7 kernel: 9 tiles x 28 x 2)")
     ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
                     help="post-process input: COCO-like 6-person maps (default) or the random-weight "
                          "network's own last stage")
@@ -114,7 +115,7 @@ def main():
         nonlocal persons
         ctx.run_staged()
         ctx.synchronize()
-        res = [ctx.fetch_result(i) for i in range(B)]
+        res = ctx.fetch_results(0, B)
         if collect:
             persons += sum(r[2].n_persons for r in res)
         if dist is not None:

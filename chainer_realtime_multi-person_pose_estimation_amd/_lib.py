@@ -22,7 +22,7 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
-    "op_set_precision", "op_get_precision",
+    "op_set_precision", "op_get_precision", "op_fetch_results",
 )
 PRECISION = {"fp32": 0, "bf16x3": 1}
 
@@ -93,6 +93,7 @@ def lib():
         "op_profile_reset": ([P], ctypes.c_int),
         "op_set_precision": ([P, I32], ctypes.c_int),
         "op_get_precision": ([P, P], ctypes.c_int),
+        "op_fetch_results": ([P, I32, I32, P, P, I32, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -317,6 +318,15 @@ class Context(object):
         check(lib().op_fetch_result(self.h, int(frame), ptr(poses), ptr(scores), cap, ctypes.byref(res)),
               "op_fetch_result")
         return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    def fetch_results(self, first, n, cap=64):
+        """Results of staged frames [first, first+n) in three copies: [(poses, scores, res), ...]."""
+        poses = np.empty((n, cap, N_JOINTS, 3), np.float64)
+        scores = np.empty((n, cap), np.float64)
+        res = (OpFrameResult * n)()
+        check(lib().op_fetch_results(self.h, int(first), int(n), ptr(poses), ptr(scores), cap, res),
+              "op_fetch_results")
+        return [(poses[i, :res[i].n_persons].copy(), scores[i, :res[i].n_persons].copy(), res[i]) for i in range(n)]
 
     def last_timing(self):
         a, b, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()

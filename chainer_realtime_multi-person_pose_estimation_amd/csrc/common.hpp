@@ -12,6 +12,18 @@ namespace op {
 // Thread-local last error text for op_last_error().
 void set_error(const std::string& msg);
 
+// OP_DEBUG_SYNC=1: synchronise after every kernel launch (outside graph capture) and report the
+// kernel a fault happened in.
+extern bool g_debug_sync;
+int debug_after_launch(const char* name, hipStream_t st);
+#define OP_AFTER_LAUNCH(name, st)                         \
+  do {                                                    \
+    if (::op::g_debug_sync) {                             \
+      int _r = ::op::debug_after_launch((name), (st));    \
+      if (_r) return _r;                                  \
+    }                                                     \
+  } while (0)
+
 #define OP_HIP_CHECK(expr)                                                                   \
   do {                                                                                       \
     hipError_t _e = (expr);                                                                  \
@@ -66,8 +78,14 @@ struct SplitConvGroup {
 };
 struct SplitConvShape {
   int32_t n, h, w, pin, cs_in, pout, cs_out, c16, ks, relu, groups, cs_out32;
+  int32_t halo_mode;  // 0 gather kernel; 7x7 only: 1 shared-weight halo (x1 buffer), 2 (x2 buffers); 3 co-split halo (all)
 };
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st);
+// co-split halo kernel (conv_halo.hip): tile of tr rows x tc cols per workgroup, nh 1-KiB halo pieces per plane
+struct HaloTiling {
+  int32_t tr, tc, tiles_y, tiles_x, nh;
+};
+int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
                           int32_t c, hipStream_t st);
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);
@@ -95,6 +113,8 @@ struct PostBuffers {
   int32_t* peak_xy;    // [B][18][maxp]  x | y << 16
   float* peak_score;   // [B][18][maxp]
   int32_t* peak_cnt;   // [B][18]
+  int32_t* stage_key;  // [B][18][maxp] unordered peaks (y*mw + x) before peak_sort
+  float* stage_score;  // [B][18][maxp]
   double* cand_score;  // [B][19][maxc]
   int32_t* cand_idx;   // [B][19][maxc]
   int32_t* cand_cnt;   // [B][19]

@@ -137,6 +137,7 @@ static int launch_conv_t(const ConvShape& s, const ConvGroup* g, hipStream_t st)
   dim3 grid((unsigned)((total + 4 * PB * 32 - 1) / (4 * PB * 32)), (unsigned)((cop_max + CB * 32 - 1) / (CB * 32)),
             (unsigned)s.groups);
   hipLaunchKernelGGL((conv_mfma_f32<KS, CB, PB>), grid, dim3(256), 0, st, s, g[0], s.groups > 1 ? g[1] : g[0]);
+  OP_AFTER_LAUNCH("conv_mfma_f32<KS", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -197,6 +198,7 @@ int launch_maxpool2(const float* in, int32_t pin, float* out, int32_t pout, int3
   const int64_t total = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
   hipLaunchKernelGGL(maxpool2_nhwc, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, pin, out, pout, n,
                      h, w, c / 4);
+  OP_AFTER_LAUNCH("maxpool2_nhwc", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -227,6 +229,7 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc8(const float* __restrict__ x
 int launch_nchw_to_nhwc8(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st) {
   const int64_t total = (int64_t)n * (h + 2) * (w + 2);
   hipLaunchKernelGGL(nchw_to_nhwc8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, out, n, h, w);
+  OP_AFTER_LAUNCH("nchw_to_nhwc8", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -252,6 +255,7 @@ __global__ __launch_bounds__(256) void extract_maps(const float* __restrict__ ca
 int launch_extract_maps(const float* cat, int32_t n, int32_t h, int32_t w, float* paf, float* heat, hipStream_t st) {
   const int64_t total = (int64_t)n * 57 * h * w;
   hipLaunchKernelGGL(extract_maps, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cat, n, h, w, paf, heat);
+  OP_AFTER_LAUNCH("extract_maps", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -286,6 +290,7 @@ int launch_preprocess(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
   const int64_t total = (int64_t)n * (dh + 2) * (dw + 2);
   hipLaunchKernelGGL(preprocess_nhwc8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, frames, frame_bytes,
                      row_stride, n, sh, sw, dh, dw, out);
+  OP_AFTER_LAUNCH("preprocess_nhwc8", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -307,6 +312,7 @@ int launch_preprocess_planar(const uint8_t* bgr, int64_t row_stride, int32_t sh,
   const int64_t total = (int64_t)dh * dw;
   hipLaunchKernelGGL(preprocess_planar, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, bgr, row_stride, sh,
                      sw, dh, dw, out_nchw);
+  OP_AFTER_LAUNCH("preprocess_planar", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }

@@ -9,7 +9,10 @@
 //
 // Split activation format (same 4 B/element as f32, NHWC with a zero halo): per pixel, every
 // group of 8 channels is 16 B of hi followed by 16 B of lo.  The producing conv's epilogue writes
-// it directly; weights are pre-split on the host and packed [c16][tap][co][k-half][hi8 lo8].
+// it directly.  Weights are pre-split on the host and packed in four planes per (c16, tap):
+// [c16][tap][plane = 2*k-half + (hi|lo)][co][8 bf16], so a wave's A-operand reads (lanes = 32
+// consecutive channels, 16 B apart) are LDS-bank-conflict-free.  The pixel operand rows are
+// XOR-swizzled per 16-B part on the gather side (part ^ ((px >> 2) & 3)) for the same reason.
 //
 // Workgroup = 4 waves; wave w owns CB x PB blocks of 32 output channels x 32 pixels; the 4 waves
 // share the channel tile.  Per (tap, 16-channel) step the workgroup stages the weight tile
@@ -27,117 +30,19 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int KS, int CB, int PB>
-__global__ __launch_bounds__(256, 2) void conv_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1) {
-  constexpr int KSQ = KS * KS;
-  constexpr int R = KS / 2;
-  constexpr int W_BYTES = CB * 32 * 64;      // weight tile per step
-  constexpr int X_BYTES = PB * 32 * 64;      // one wave's pixel operand rows per step
-  constexpr int STAGE = W_BYTES + 4 * X_BYTES;
-  constexpr int NX = PB * 2;                 // glds per wave for X (16 pixels x 64 B each)
-  constexpr int NW = W_BYTES / 4096;         // glds per wave for W (4 waves x 1 KiB each)
-  static_assert(W_BYTES % 4096 == 0, "CB must be a multiple of 2");
-  __shared__ __attribute__((aligned(16))) char lds[3 * STAGE];
-
-  const SplitConvGroup g = blockIdx.z == 0 ? g0 : g1;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int co_base = blockIdx.y * (CB * 32);
-  if (co_base >= g.cop) return;  // whole workgroup
-  const int hw = s.h * s.w;
-  const int total = s.n * hw;
-  const int px_base = (blockIdx.x * 4 + wave) * (PB * 32);
-  const int wp_in = s.w + 2 * s.pin;
-  const int hp_in = s.h + 2 * s.pin;
-  const int64_t in_pix_bytes = (int64_t)s.cs_in * 4;
-
-  // per-lane gather sources: X glds i, lane L -> pixel px_base + i*16 + (L>>2), part (L&3)
-  const char* xsrc[NX];
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    int p = px_base + i * 16 + (lane >> 2);
-    if (p >= total) p = total - 1;
-    const int n = p / hw;
-    const int rem = p - n * hw;
-    const int y = rem / s.w;
-    const int x = rem - y * s.w;
-    xsrc[i] = (const char*)g.in + ((int64_t)(n * hp_in + y + s.pin - R) * wp_in + (x + s.pin - R)) * in_pix_bytes +
-              (lane & 3) * 16;
-  }
-  const char* wsrc = (const char*)g.w + (int64_t)co_base * 64 + (wave * NW * 1024) + lane * 16;
-  const int64_t wstep = (int64_t)g.cop * 64;
-  const int n_it = s.c16 * KSQ;
-
-  auto stage = [&](int it, int buf) {
-    const int c = it / KSQ;
-    const int t = it - c * KSQ;
-    const int ky = t / KS;
-    const int kx = t - ky * KS;
-    const int64_t xoff = ((int64_t)ky * wp_in + kx) * in_pix_bytes + c * 64;
-    char* base = lds + buf * STAGE;
-#pragma unroll
-    for (int j = 0; j < NW; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)it * wstep + j * 1024),
-                                       LDS_PTR(base + (wave * NW + j) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < NX; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(xsrc[i] + xoff), LDS_PTR(base + W_BYTES + wave * X_BYTES + i * 1024),
-                                       16, 0, 0);
-  };
-
-  floatx16 acc[CB][PB];
-#pragma unroll
-  for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[cb][pb][r] = 0.0f;
-
+// Epilogue shared by the split kernels: bias, ReLU, split store (+ optional dense f32 copy).
+// Lane holds pixel (lane & 31) of each 32-pixel block and, per register group q, output
+// channels 8q + 4*(lane>>5) .. +3 of each 32-channel block (32x32 C/D map).
+template <int CB, int PB>
+__device__ __forceinline__ void store_tile(const SplitConvShape& s, const SplitConvGroup& g, floatx16 (&acc)[CB][PB],
+                                           int co_base, int px_base, int total, int hw, int lane) {
   const int l32 = lane & 31, hi = lane >> 5;
-  stage(0, 0);
-  if (n_it > 1) stage(1, 1);
-  int buf = 0;
-  for (int it = 0; it < n_it; ++it) {
-    // this wave's copies for step `it` have landed once at most one younger stage is in flight
-    if (it + 1 < n_it)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW + NX) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's copies for `it` landed; everyone is done with it-1
-    asm volatile("" ::: "memory");  // keep the next stage's LDS writes and this step's reads below the barrier
-    if (it + 2 < n_it) stage(it + 2, buf == 0 ? 2 : buf - 1);
-    const char* base = lds + buf * STAGE;
-    bf16x8 ah[CB], al[CB], bh[PB], bl[PB];
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      const char* a = base + (cb * 32 + l32) * 64 + hi * 32;
-      ah[cb] = *(const bf16x8*)a;
-      al[cb] = *(const bf16x8*)(a + 16);
-    }
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb) {
-      const char* b = base + W_BYTES + wave * X_BYTES + (pb * 32 + l32) * 64 + hi * 32;
-      bh[pb] = *(const bf16x8*)b;
-      bl[pb] = *(const bf16x8*)(b + 16);
-    }
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) {
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[pb], acc[cb][pb], 0, 0, 0);
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[pb], acc[cb][pb], 0, 0, 0);
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[pb], acc[cb][pb], 0, 0, 0);
-      }
-    buf = buf == 2 ? 0 : buf + 1;
-  }
-
-  // Epilogue: lane holds pixel l32 and, per register group q, channels 8q + 4hi .. +3 of each block.
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) {
     const int p = px_base + pb * 32 + l32;
-    if (p >= total) continue;
+    if (p < 0 || p >= total) continue;
     const int n = p / hw;
     const int rem = p - n * hw;
     const int y = rem / s.w;
@@ -173,15 +78,135 @@ __global__ __launch_bounds__(256, 2) void conv_bf16x3(SplitConvShape s, SplitCon
 }
 
 template <int KS, int CB, int PB>
+__global__ __launch_bounds__(256, 2) void conv_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1) {
+  constexpr int KSQ = KS * KS;
+  constexpr int R = KS / 2;
+  constexpr int W_BYTES = CB * 32 * 64;      // weight tile per step
+  constexpr int X_BYTES = PB * 32 * 64;      // one wave's pixel operand rows per step
+  constexpr int STAGE = W_BYTES + 4 * X_BYTES;
+  constexpr int NX = PB * 2;                 // glds per wave for X (16 pixels x 64 B each)
+  constexpr int NW = W_BYTES / 4096;         // glds per wave for W (4 waves x 1 KiB each)
+  static_assert(W_BYTES % 4096 == 0, "CB must be a multiple of 2");
+  __shared__ __attribute__((aligned(16))) char lds[3 * STAGE];
+
+  const SplitConvGroup g = blockIdx.z == 0 ? g0 : g1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int co_base = blockIdx.y * (CB * 32);
+  if (co_base >= g.cop) return;  // whole workgroup
+  const int hw = s.h * s.w;
+  const int total = s.n * hw;
+  const int px_base = (blockIdx.x * 4 + wave) * (PB * 32);
+  const int wp_in = s.w + 2 * s.pin;
+  const int hp_in = s.h + 2 * s.pin;
+  const int64_t in_pix_bytes = (int64_t)s.cs_in * 4;
+
+  // per-lane gather sources: X glds i, lane L -> pixel px_base + i*16 + (L>>2), part (L&3)
+  const char* xsrc[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    int p = px_base + i * 16 + (lane >> 2);
+    if (p >= total) p = total - 1;
+    const int n = p / hw;
+    const int rem = p - n * hw;
+    const int y = rem / s.w;
+    const int x = rem - y * s.w;
+    // LDS slot (lane & 3) of pixel (i*16 + lane/4) holds global part (slot ^ ((px >> 2) & 3))
+    const int pl = i * 16 + (lane >> 2);
+    xsrc[i] = (const char*)g.in + ((int64_t)(n * hp_in + y + s.pin - R) * wp_in + (x + s.pin - R)) * in_pix_bytes +
+              (((lane & 3) ^ ((pl >> 2) & 3)) * 16);
+  }
+  // weight pieces: piece k (= wave*NW + j) -> plane k / (CB/2), 64-channel half k % (CB/2)
+  const char* wsrc[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int k = wave * NW + j;
+    wsrc[j] = (const char*)g.w + ((int64_t)(k / (CB / 2)) * g.cop + co_base + (k % (CB / 2)) * 64 + lane) * 16;
+  }
+  const int64_t wstep = (int64_t)g.cop * 64;
+  const int n_it = s.c16 * KSQ;
+
+  auto stage = [&](int it, int buf) {
+    const int c = it / KSQ;
+    const int t = it - c * KSQ;
+    const int ky = t / KS;
+    const int kx = t - ky * KS;
+    const int64_t xoff = ((int64_t)ky * wp_in + kx) * in_pix_bytes + c * 64;
+    char* base = lds + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[j] + (int64_t)it * wstep),
+                                       LDS_PTR(base + (wave * NW + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(xsrc[i] + xoff), LDS_PTR(base + W_BYTES + wave * X_BYTES + i * 1024),
+                                       16, 0, 0);
+  };
+
+  floatx16 acc[CB][PB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[cb][pb][r] = 0.0f;
+
+  const int l32 = lane & 31, hi = lane >> 5;
+  stage(0, 0);
+  if (n_it > 1) stage(1, 1);
+  int buf = 0;
+  for (int it = 0; it < n_it; ++it) {
+    // this wave's copies for step `it` have landed once at most one younger stage is in flight
+    if (it + 1 < n_it)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW + NX) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's copies for `it` landed; everyone is done with it-1
+    asm volatile("" ::: "memory");  // keep the next stage's LDS writes and this step's reads below the barrier
+    if (it + 2 < n_it) stage(it + 2, buf == 0 ? 2 : buf - 1);
+    const char* base = lds + buf * STAGE;
+    bf16x8 ah[CB], al[CB], bh[PB], bl[PB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const char* a = base + (2 * hi) * (CB * 512) + (cb * 32 + l32) * 16;
+      ah[cb] = *(const bf16x8*)a;
+      al[cb] = *(const bf16x8*)(a + CB * 512);
+    }
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      const int pl = pb * 32 + l32;
+      const char* b = base + W_BYTES + wave * X_BYTES + pl * 64;
+      const int sw = (pl >> 2) & 3;
+      bh[pb] = *(const bf16x8*)(b + (((2 * hi) ^ sw) * 16));
+      bl[pb] = *(const bf16x8*)(b + (((2 * hi + 1) ^ sw) * 16));
+    }
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) {
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[pb], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[pb], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[pb], acc[cb][pb], 0, 0, 0);
+      }
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+
+  store_tile<CB, PB>(s, g, acc, co_base, px_base, total, hw, lane);
+}
+
+template <int KS, int CB, int PB>
 static int launch_bf16x3_t(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st) {
   const int64_t total = (int64_t)s.n * s.h * s.w;
   const int cop_max = s.groups > 1 ? (g[0].cop > g[1].cop ? g[0].cop : g[1].cop) : g[0].cop;
   dim3 grid((unsigned)((total + 4 * PB * 32 - 1) / (4 * PB * 32)), (unsigned)((cop_max + CB * 32 - 1) / (CB * 32)),
             (unsigned)s.groups);
   hipLaunchKernelGGL((conv_bf16x3<KS, CB, PB>), grid, dim3(256), 0, st, s, g[0], s.groups > 1 ? g[1] : g[0]);
+  OP_AFTER_LAUNCH("conv_bf16x3<KS", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
+
+int launch_conv7_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st) {
   if (s.c16 <= 0 || (s.ks != 1 && s.ks != 3 && s.ks != 7) || s.pin < s.ks / 2 || s.cs_in % 16 || s.cs_out % 8) {
@@ -196,6 +221,16 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     }
     if (g[i].cop % 128) wide = false;
   }
+  if (s.halo_mode == 3) {  // co-split halo kernel (conv_halo.hip), every kernel size
+    int taken = 0;
+    const int rc = launch_conv_halo(s, g, st, &taken);
+    if (rc || taken) return rc;
+  }
+  if (s.ks == 7 && (s.halo_mode == 1 || s.halo_mode == 2)) {
+    int taken = 0;
+    const int rc = launch_conv7_halo(s, g, st, &taken);
+    if (rc || taken) return rc;
+  }
   if (wide) {
     switch (s.ks) {
       case 1: return launch_bf16x3_t<1, 4, 2>(s, g, st);
@@ -208,6 +243,203 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     case 3: return launch_bf16x3_t<3, 2, 2>(s, g, st);
     default: return launch_bf16x3_t<7, 2, 2>(s, g, st);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 7x7 stage convs with an LDS halo (the dominant kernel: Mconv1..5 of stages 2-6, 68 % of FLOPs).
+//
+// Workgroup tile = CB*32 output channels x up to 256 consecutive pixels of ONE frame (4 waves x
+// 2 blocks of 32).  For each 16-channel chunk the workgroup stages the tile's input rows plus the
+// 3-pixel halo -- a contiguous run of padded rows of the stacked NHWC buffer -- into LDS once, and
+// all 49 taps read their shifted windows from it (reuse ~19x instead of a per-tap gather).  The
+// halo is stored as 4 planes (hi/lo x k-half) of 16 B per pixel (wave w copies plane w), so a
+// wave's B-operand reads are consecutive 16-B slots: conflict-free.  Weights stream through a
+// 3-deep ring of (tap, chunk) tiles; the next chunk's halo is copied into the second buffer
+// during the current chunk.  Every copy is global_load_lds; per step one counted vmcnt + one
+// raw s_barrier.  vmcnt accounting (per wave, issue order): step it issues W(it+2) then, on tap
+// 0, the halo of the next chunk (NH pieces), so W(it) has NW ops after it, plus NH when
+// tap(it) is 1 or 2.
+template <int CB, int NH, bool DH>
+__global__ __launch_bounds__(256, DH ? 1 : 2) void conv7_halo_bf16x3(SplitConvShape s, SplitConvGroup g0,
+                                                                      SplitConvGroup g1, int tiles_per_frame) {
+  constexpr int KS = 7, KSQ = 49, R = 3, PB = 2;
+  constexpr int W_BYTES = CB * 32 * 64;
+  constexpr int NW = W_BYTES / 4096;
+  constexpr int HALO_PLANE = NH * 1024;
+  constexpr int HALO_BYTES = 4 * HALO_PLANE;
+  constexpr int NHB = DH ? 2 : 1;  // halo buffers
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo NHB][W ring 3]
+
+  const SplitConvGroup g = blockIdx.z == 0 ? g0 : g1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int co_base = blockIdx.y * (CB * 32);
+  if (co_base >= g.cop) return;
+  const int hw = s.h * s.w;
+  const int total = s.n * hw;
+  const int frame = blockIdx.x / tiles_per_frame;
+  const int tile_px0 = (blockIdx.x - frame * tiles_per_frame) * 256;  // within the frame
+  const int wp = s.w + 2 * R;
+  const int hp = s.h + 2 * R;
+  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
+  // halo = padded rows [y_first, y_last + 6] of this frame (padded-row coordinates)
+  const int y_first = tile_px0 / s.w;
+  int last_px = tile_px0 + 255;
+  if (last_px >= hw) last_px = hw - 1;
+  const int y_last = last_px / s.w;
+  const int hrows = y_last - y_first + KS;
+  const int npix = hrows * wp;  // <= NH * 64 by construction (host check)
+  const char* hsrc0 = (const char*)g.in + ((int64_t)(frame * hp + y_first) * wp) * pix_bytes + wave * 16;
+
+  // weight pieces: piece k = wave*NW + j -> plane k / (CB/2), 64-channel half k % (CB/2)
+  const char* wsrc[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int k = wave * NW + j;
+    wsrc[j] = (const char*)g.w + ((int64_t)(k / (CB / 2)) * g.cop + co_base + (k % (CB / 2)) * 64 + lane) * 16;
+  }
+  const int64_t wstep = (int64_t)g.cop * 64;
+  const int n_it = s.c16 * KSQ;
+
+  // this lane's output pixels -> halo pixel index of tap (0,0)
+  const int l32 = lane & 31, hi = lane >> 5;
+  int q0[PB];
+  const int px_base = frame * hw + tile_px0 + wave * (PB * 32);
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    int pf = tile_px0 + wave * (PB * 32) + pb * 32 + l32;  // within the frame
+    if (pf >= hw) pf = hw - 1;
+    const int y = pf / s.w, x = pf - (pf / s.w) * s.w;
+    q0[pb] = (y - y_first) * wp + x;
+  }
+
+  auto stage_w = [&](int it) {
+    char* base = lds + NHB * HALO_BYTES + (it % 3) * W_BYTES;  // slot of the unclamped step: never read again
+    if (it >= n_it) it = n_it - 1;  // keep the per-step op count uniform (the copy is never consumed)
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[j] + (int64_t)it * wstep), LDS_PTR(base + (wave * NW + j) * 1024),
+                                       16, 0, 0);
+  };
+  auto stage_halo = [&](int c) {
+    char* base = lds + (DH ? (c & 1) : 0) * HALO_BYTES + wave * HALO_PLANE;  // buffer of the unclamped chunk
+    if (c >= s.c16) c = s.c16 - 1;  // uniform op count; that copy is never read
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      int q = i * 64 + lane;
+      if (q >= npix) q = npix - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(hsrc0 + (int64_t)q * pix_bytes + c * 64), LDS_PTR(base + i * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  floatx16 acc[CB][PB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[cb][pb][r] = 0.0f;
+
+  if (DH) stage_halo(0);
+  stage_w(0);
+  stage_w(1);
+  int c = 0, t = 0;
+  for (int it = 0; it < n_it; ++it) {
+    if (DH && (t == 1 || t == 2))
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW + NH) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (!DH && t == 0) {
+      // single halo buffer: everyone finished the previous chunk (barrier above); load this chunk's
+      // halo, wait for it (W(it+1) is waited for too), and publish it with a second barrier
+      stage_halo(c);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    stage_w(it + 2);
+    if (DH && t == 0) stage_halo(c + 1);
+    const char* wb = lds + NHB * HALO_BYTES + (it % 3) * W_BYTES;
+    const char* hb = lds + (DH ? (c & 1) : 0) * HALO_BYTES;
+    const int ky = t / KS, kx = t - (t / KS) * KS;
+    const int toff = ky * wp + kx;
+    bf16x8 ah[CB], al[CB], bh[PB], bl[PB];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      const char* b = hb + (q0[pb] + toff) * 16;
+      bh[pb] = *(const bf16x8*)(b + (2 * hi) * HALO_PLANE);
+      bl[pb] = *(const bf16x8*)(b + (2 * hi + 1) * HALO_PLANE);
+    }
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const char* a = wb + (2 * hi) * (CB * 512) + (cb * 32 + l32) * 16;
+      ah[cb] = *(const bf16x8*)a;
+      al[cb] = *(const bf16x8*)(a + CB * 512);
+    }
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) {
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[pb], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[pb], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[pb], acc[cb][pb], 0, 0, 0);
+      }
+    if (++t == KSQ) {
+      t = 0;
+      ++c;
+    }
+  }
+  // pixels past the end of this frame are masked by the tile bound
+  const int frame_end = frame * hw + hw;
+  store_tile<CB, PB>(s, g, acc, co_base, px_base, frame_end < total ? frame_end : total, hw, lane);
+}
+
+// Halo pieces per wave needed for a 256-pixel tile at width w (7x7, pad 3).
+static int halo_pieces(int w) {
+  const int rows = (255 + w - 1) / w + 1 + 6;  // rows spanned by 256 consecutive pixels + halo
+  return (rows * (w + 6) + 63) / 64;
+}
+
+template <int CB, int NH, bool DH>
+static int launch_halo_t(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st) {
+  const int hw = s.h * s.w;
+  const int tpf = (hw + 255) / 256;
+  const int cop_max = s.groups > 1 ? (g[0].cop > g[1].cop ? g[0].cop : g[1].cop) : g[0].cop;
+  const size_t lds = (DH ? 2 : 1) * 4 * NH * 1024 + 3 * CB * 32 * 64;
+  static bool attr_set = false;
+  if (!attr_set) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv7_halo_bf16x3<CB, NH, DH>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = true;
+  }
+  dim3 grid((unsigned)(s.n * tpf), (unsigned)((cop_max + CB * 32 - 1) / (CB * 32)), (unsigned)s.groups);
+  hipLaunchKernelGGL((conv7_halo_bf16x3<CB, NH, DH>), grid, dim3(256), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0],
+                     tpf);
+  OP_AFTER_LAUNCH("conv7_halo_bf16x3<CB", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// Returns 1 if the halo kernel took the launch, 0 if the shape needs the generic kernel.
+int launch_conv7_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
+  *taken = 0;
+  if (s.ks != 7 || s.pin != 3 || s.cs_in % 16) return OP_OK;
+  for (int i = 0; i < s.groups; ++i)
+    if (g[i].cop % 128 || g[i].cin_off % 16) return OP_OK;
+  const int nh = halo_pieces(s.w);
+  *taken = 1;
+  if (s.halo_mode == 2) {  // double-buffered halo, 1 workgroup per CU
+    if (nh <= 12) return launch_halo_t<4, 12, true>(s, g, st);
+    if (nh <= 16) return launch_halo_t<4, 16, true>(s, g, st);
+  } else {  // single halo buffer, 2 workgroups per CU
+    if (nh <= 12) return launch_halo_t<4, 12, false>(s, g, st);
+    if (nh <= 16) return launch_halo_t<4, 16, false>(s, g, st);
+  }
+  *taken = 0;
+  return OP_OK;
 }
 
 // ---- split-format helpers ----
@@ -286,6 +518,7 @@ int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout
   const int64_t total = (int64_t)n * (h / 2) * (w / 2) * (c / 8);
   hipLaunchKernelGGL(maxpool2_split, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const char*)in, pin,
                      (char*)out, pout, n, h, w, c / 8);
+  OP_AFTER_LAUNCH("maxpool2_split", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -316,6 +549,7 @@ __global__ __launch_bounds__(256) void nchw_to_split16(const float* __restrict__
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st) {
   const int64_t total = (int64_t)n * (h + 2) * (w + 2);
   hipLaunchKernelGGL(nchw_to_split16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, (char*)out, n, h, w);
+  OP_AFTER_LAUNCH("nchw_to_split16", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -347,6 +581,7 @@ int launch_preprocess_split(const uint8_t* frames, int64_t frame_bytes, int64_t 
   const int64_t total = (int64_t)n * (dh + 2) * (dw + 2);
   hipLaunchKernelGGL(preprocess_split16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, frames, frame_bytes,
                      row_stride, n, sh, sw, dh, dw, (char*)out);
+  OP_AFTER_LAUNCH("preprocess_split16", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -373,6 +608,7 @@ int launch_extract_maps32(const float* m, int32_t cs, int32_t heat_off, int32_t 
   const int64_t total = (int64_t)n * 57 * h * w;
   hipLaunchKernelGGL(extract_maps32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, m, cs, heat_off, n, h, w,
                      paf, heat);
+  OP_AFTER_LAUNCH("extract_maps32", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }

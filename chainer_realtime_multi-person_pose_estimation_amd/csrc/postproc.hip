@@ -1,11 +1,11 @@
 // PAF post-process kernels for gfx950 (pose_detector.py:75-265, 501-517).
 //
 // Bit-exact restatement of the reference CPU path (the parity target):
-//   upsample_heat   F.resize_images align-corners bilinear, f64 weights cast to f32      :501-502
-//   gauss_v/gauss_h scipy gaussian_filter(sigma 2.5): reflect, 21 taps, f64 accumulate in
-//                   NI_Correlate1D's symmetric order, f32 store between the two passes    :86
-//   nms_compact     strict 4-neighbour NMS, peaks ordered (joint, y, x) by a block-wide
-//                   ordered (ballot + prefix) compaction                                  :87-110
+//   heat_vpass      F.resize_images align-corners bilinear (f64 weights cast to f32) fused
+//                   with scipy gaussian_filter's axis-0 pass: reflect, 21 taps, f64
+//                   accumulate in NI_Correlate1D's symmetric order, f32 store           :501-502, :86
+//   heat_hpass_nms  axis-1 pass + strict 4-neighbour NMS on an LDS tile                  :86-102
+//   peak_sort       restores np.nonzero's row-major peak order per (frame, joint)        :104-108
 //   limb_pairs      line integral over 10 linspace points, np.round half-to-even, PAF
 //                   samples recomputed with the upsample formula (no full-res PAF write),
 //                   fma(px,ux, py*uy) dot, NumPy pairwise sum                             :135-157
@@ -89,20 +89,6 @@ __device__ __forceinline__ float up_sample(const LowMap& m, int c, const UpTap& 
                     m.at(c, t.v0 + 1, t.u0 + 1));
 }
 
-// heat channels 0..17 (the background channel 18 is dropped, pose_detector.py:78) -> up[f][j][y][x]
-__global__ __launch_bounds__(256) void upsample_heat(MapSource src, PostShape s, float* __restrict__ up) {
-  const int64_t plane = (int64_t)s.mh * s.mw;
-  const int64_t total = (int64_t)s.n * OP_N_JOINTS * plane;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int ox = (int)(i % s.mw);
-  const int oy = (int)((i / s.mw) % s.mh);
-  const int j = (int)((i / plane) % OP_N_JOINTS);
-  const int f = (int)(i / (plane * OP_N_JOINTS));
-  const UpTap t = up_tap(oy, ox, s.lh, s.lw, s.mh, s.mw);
-  up[i] = up_sample(low_map(src, s.lw, f), src.heat_off + j, t);
-}
-
 // Chainer resize for a planar (c,h,w) tensor (stage-level ABI).
 __global__ __launch_bounds__(256) void resize_planar(const float* __restrict__ x, int c, int h, int w, int oh, int ow,
                                                      float* __restrict__ y) {
@@ -116,92 +102,6 @@ __global__ __launch_bounds__(256) void resize_planar(const float* __restrict__ x
   const float* p = x + (int64_t)cc * h * w;
   y[i] = up_combine(t, p[t.v0 * w + t.u0], p[t.v0 * w + t.u0 + 1], p[(t.v0 + 1) * w + t.u0],
                     p[(t.v0 + 1) * w + t.u0 + 1]);
-}
-
-__device__ __forceinline__ int reflect_index(int i, int L) {
-  const int p = 2 * L;
-  i %= p;
-  if (i < 0) i += p;
-  if (i >= L) i = p - 1 - i;
-  return i;
-}
-
-// NI_Correlate1D symmetric branch along y (axis 0): o = x0*w0; o += (x[-k] + x[+k]) * w[-k] for k = r..1.
-__global__ __launch_bounds__(256) void gauss_v(const float* __restrict__ in, float* __restrict__ out, int nplanes,
-                                               int H, int W, const double* __restrict__ w, int r) {
-  const int64_t plane = (int64_t)H * W;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= plane * nplanes) return;
-  const int x = (int)(i % W);
-  const int y = (int)((i / W) % H);
-  const float* p = in + (i / plane) * plane;
-  double o = __dmul_rn((double)p[(int64_t)y * W + x], w[r]);
-  for (int jj = -r; jj < 0; ++jj) {
-    const double a = (double)p[(int64_t)reflect_index(y + jj, H) * W + x];
-    const double b = (double)p[(int64_t)reflect_index(y - jj, H) * W + x];
-    o = __dadd_rn(o, __dmul_rn(__dadd_rn(a, b), w[r + jj]));
-  }
-  out[i] = __double2float_rn(o);
-}
-
-// Same along x (axis 1), one row per 256-thread block chunk.
-__global__ __launch_bounds__(256) void gauss_h(const float* __restrict__ in, float* __restrict__ out, int nplanes, int H,
-                                               int W, const double* __restrict__ w, int r) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)H * W * nplanes) return;
-  const int x = (int)(i % W);
-  const float* row = in + (i / W) * W;
-  double o = __dmul_rn((double)row[x], w[r]);
-  for (int jj = -r; jj < 0; ++jj) {
-    const double a = (double)row[reflect_index(x + jj, W)];
-    const double b = (double)row[reflect_index(x - jj, W)];
-    o = __dadd_rn(o, __dmul_rn(__dadd_rn(a, b), w[r + jj]));
-  }
-  out[i] = __double2float_rn(o);
-}
-
-// Strict 4-neighbour NMS + ordered compaction, one 256-thread block per (frame, joint).
-__global__ __launch_bounds__(256) void nms_compact(const float* __restrict__ hm, int H, int W, float thresh, int maxp,
-                                                   int32_t* __restrict__ peak_xy, float* __restrict__ peak_score,
-                                                   int32_t* __restrict__ peak_cnt) {
-  __shared__ int wave_cnt[4];
-  __shared__ int running;
-  const int fj = blockIdx.x;  // frame * 18 + joint
-  const float* m = hm + (int64_t)fj * H * W;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) running = 0;
-  __syncthreads();
-  const int64_t total = (int64_t)H * W;
-  for (int64_t base = 0; base < total; base += 256) {
-    const int64_t p = base + tid;
-    bool pk = false;
-    float v = 0.0f;
-    int x = 0, y = 0;
-    if (p < total) {
-      y = (int)(p / W);
-      x = (int)(p - (int64_t)y * W);
-      v = m[p];
-      const float up = y > 0 ? m[p - W] : 0.0f;
-      const float dn = y < H - 1 ? m[p + W] : 0.0f;
-      const float lf = x > 0 ? m[p - 1] : 0.0f;
-      const float rt = x < W - 1 ? m[p + 1] : 0.0f;
-      pk = v > thresh && v > up && v > dn && v > lf && v > rt;
-    }
-    const unsigned long long bal = __ballot(pk);
-    if (lane == 0) wave_cnt[wave] = __popcll(bal);
-    __syncthreads();
-    int before = running;
-    for (int q = 0; q < wave; ++q) before += wave_cnt[q];
-    const int pos = before + __popcll(bal & ((1ull << lane) - 1ull));
-    if (pk && pos < maxp) {
-      peak_xy[(int64_t)fj * maxp + pos] = x | (y << 16);
-      peak_score[(int64_t)fj * maxp + pos] = v;
-    }
-    __syncthreads();
-    if (tid == 0) running += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
-    __syncthreads();
-  }
-  if (tid == 0) peak_cnt[fj] = running;  // may exceed maxp: overflow is reported per frame
 }
 
 // PAF sample at map pixel (y, x) of PAF channel c: recomputed from the low-res map with the
@@ -548,24 +448,178 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   }
 }
 
-// ---------------- launchers ----------------
-static inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+// ---- heat-map pipeline: (upsample + vertical Gaussian) -> (horizontal Gaussian + NMS) -> sort ----
+// Tiles are staged in LDS; the reflect boundary is resolved once per LDS row / column.
+constexpr int kVT = 64;   // vertical-pass tile (rows x cols)
+constexpr int kHTR = 16;  // horizontal-pass tile rows
+constexpr int kHTC = 64;  // horizontal-pass tile cols
+constexpr int kMaxR = 16; // max Gaussian radius of the tiled kernels
 
-static int run_gauss_nms(const float* src_up, const PostShape& s, PostBuffers& b, hipStream_t st) {
-  const int64_t planes = (int64_t)s.n * OP_N_JOINTS;
-  const int64_t total = planes * s.mh * s.mw;
-  hipLaunchKernelGGL(gauss_v, dim3(nblk(total)), dim3(256), 0, st, src_up, b.tmp, (int)planes, s.mh, s.mw, b.gauss_w,
-                     s.radius);
-  hipLaunchKernelGGL(gauss_h, dim3(nblk(total)), dim3(256), 0, st, b.tmp, b.hm, (int)planes, s.mh, s.mw, b.gauss_w,
-                     s.radius);
-  hipLaunchKernelGGL(nms_compact, dim3((unsigned)planes), dim3(256), 0, st, b.hm, s.mh, s.mw, s.peak_thresh, b.maxp,
-                     b.peak_xy, b.peak_score, b.peak_cnt);
+__device__ __forceinline__ int reflect_near(int i, int L) {
+  if (i < 0) i = -i - 1;
+  if (i >= L) i = 2 * L - 1 - i;
+  return i < 0 ? 0 : (i >= L ? L - 1 : i);  // L > radius: one reflection suffices
+}
+
+struct HeatLow {
+  MapSource src;
+  int lh, lw, mh, mw;
+  __device__ __forceinline__ float at(int f, int j, int y, int x) const {
+    return up_sample(low_map(src, lw, f), src.heat_off + j, up_tap(y, x, lh, lw, mh, mw));
+  }
+};
+struct HeatFull {  // already-upsampled planes [f*18 + j][mh][mw]
+  const float* p;
+  int mh, mw;
+  __device__ __forceinline__ float at(int f, int j, int y, int x) const {
+    return p[(((int64_t)f * OP_N_JOINTS + j) * mh + y) * mw + x];
+  }
+};
+
+template <class Src>
+__global__ __launch_bounds__(256) void heat_vpass(Src src, int mh, int mw, const double* __restrict__ w, int r,
+                                                  float* __restrict__ tmp) {
+  __shared__ float tile[kVT + 2 * kMaxR][kVT];
+  const int fj = blockIdx.z;
+  const int f = fj / OP_N_JOINTS, j = fj - f * OP_N_JOINTS;
+  const int x0 = blockIdx.x * kVT, y0 = blockIdx.y * kVT;
+  const int rows = kVT + 2 * r;
+  for (int i = threadIdx.x; i < rows * kVT; i += 256) {
+    const int ly = i / kVT, lx = i - ly * kVT;
+    const int x = x0 + lx;
+    float v = 0.0f;
+    if (x < mw) v = src.at(f, j, reflect_near(y0 - r + ly, mh), x);
+    tile[ly][lx] = v;
+  }
+  __syncthreads();
+  const int lx = threadIdx.x & (kVT - 1);
+  const int x = x0 + lx;
+  if (x >= mw) return;
+  for (int ly = threadIdx.x / kVT; ly < kVT; ly += 256 / kVT) {
+    const int y = y0 + ly;
+    if (y >= mh) break;
+    double o = __dmul_rn((double)tile[ly + r][lx], w[r]);
+    for (int jj = -r; jj < 0; ++jj)
+      o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)tile[ly + r + jj][lx], (double)tile[ly + r - jj][lx]), w[r + jj]));
+    tmp[((int64_t)fj * mh + y) * mw + x] = __double2float_rn(o);
+  }
+}
+
+// Horizontal pass + strict 4-neighbour NMS on a kHTR x kHTC tile; peaks are appended to the
+// (frame, joint) staging list as (y*mw + x, score) -- order restored by peak_sort.
+__global__ __launch_bounds__(256) void heat_hpass_nms(const float* __restrict__ tmp, int mh, int mw,
+                                                      const double* __restrict__ w, int r, float thresh, int cap,
+                                                      int32_t* __restrict__ stage_key, float* __restrict__ stage_score,
+                                                      int32_t* __restrict__ peak_cnt) {
+  __shared__ float src[kHTR + 2][kHTC + 2 + 2 * kMaxR];
+  __shared__ float hm[kHTR + 2][kHTC + 2];
+  const int fj = blockIdx.z;
+  const int x0 = blockIdx.x * kHTC, y0 = blockIdx.y * kHTR;
+  const int cols = kHTC + 2 + 2 * r;
+  const float* plane = tmp + (int64_t)fj * mh * mw;
+  for (int i = threadIdx.x; i < (kHTR + 2) * cols; i += 256) {
+    const int ly = i / cols, lx = i - ly * cols;
+    const int y = y0 - 1 + ly;
+    float v = 0.0f;
+    if (y >= 0 && y < mh) v = plane[(int64_t)y * mw + reflect_near(x0 - 1 - r + lx, mw)];
+    src[ly][lx] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (kHTR + 2) * (kHTC + 2); i += 256) {
+    const int ly = i / (kHTC + 2), lx = i - ly * (kHTC + 2);
+    const int y = y0 - 1 + ly, x = x0 - 1 + lx;
+    float v = 0.0f;  // outside the image a neighbour counts as 0 (pose_detector.py:87-94)
+    if (y >= 0 && y < mh && x >= 0 && x < mw) {
+      double o = __dmul_rn((double)src[ly][lx + r], w[r]);
+      for (int jj = -r; jj < 0; ++jj)
+        o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)src[ly][lx + r + jj], (double)src[ly][lx + r - jj]), w[r + jj]));
+      v = __double2float_rn(o);
+    }
+    hm[ly][lx] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHTR * kHTC; i += 256) {
+    const int ly = i / kHTC + 1, lx = i % kHTC + 1;
+    const int y = y0 + ly - 1, x = x0 + lx - 1;
+    if (y >= mh || x >= mw) continue;
+    const float v = hm[ly][lx];
+    if (v > thresh && v > hm[ly - 1][lx] && v > hm[ly + 1][lx] && v > hm[ly][lx - 1] && v > hm[ly][lx + 1]) {
+      const int slot = atomicAdd(peak_cnt + fj, 1);
+      if (slot < cap) {
+        stage_key[(int64_t)fj * cap + slot] = y * mw + x;
+        stage_score[(int64_t)fj * cap + slot] = v;
+      }
+    }
+  }
+}
+
+// Per (frame, joint): bitonic sort of the staged peaks by y*mw + x (= np.nonzero row-major order).
+__global__ __launch_bounds__(512) void peak_sort(const int32_t* __restrict__ stage_key,
+                                                 const float* __restrict__ stage_score, int cap, int mw,
+                                                 const int32_t* __restrict__ peak_cnt, int32_t* __restrict__ peak_xy,
+                                                 float* __restrict__ peak_score) {
+  __shared__ int32_t key[2048];
+  __shared__ float val[2048];
+  const int fj = blockIdx.x;
+  int n = peak_cnt[fj];
+  if (n > cap) n = cap;  // overflow is reported by the grouping kernel from peak_cnt
+  int m = 1;
+  while (m < n) m <<= 1;
+  for (int i = threadIdx.x; i < m; i += 512) {
+    key[i] = i < n ? stage_key[(int64_t)fj * cap + i] : 0x7fffffff;
+    val[i] = i < n ? stage_score[(int64_t)fj * cap + i] : 0.0f;
+  }
+  __syncthreads();
+  for (int k = 2; k <= m; k <<= 1)
+    for (int jb = k >> 1; jb > 0; jb >>= 1) {
+      for (int i = threadIdx.x; i < m; i += 512) {
+        const int l = i ^ jb;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          if ((key[i] > key[l]) == up) {
+            const int32_t tk = key[i];
+            key[i] = key[l];
+            key[l] = tk;
+            const float tv = val[i];
+            val[i] = val[l];
+            val[l] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < n; i += 512) {
+    const int yx = key[i];
+    const int y = yx / mw, x = yx - y * mw;
+    peak_xy[(int64_t)fj * cap + i] = x | (y << 16);
+    peak_score[(int64_t)fj * cap + i] = val[i];
+  }
+}
+
+template <class Src>
+static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
+  const int planes = s.n * OP_N_JOINTS;
+  OP_HIP_CHECK(hipMemsetAsync(b.peak_cnt, 0, sizeof(int32_t) * planes, st));
+  dim3 gv((unsigned)((s.mw + kVT - 1) / kVT), (unsigned)((s.mh + kVT - 1) / kVT), (unsigned)planes);
+  hipLaunchKernelGGL((heat_vpass<Src>), gv, dim3(256), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius, b.tmp);
+  OP_AFTER_LAUNCH("heat_vpass<Src>", st);
+  dim3 gh((unsigned)((s.mw + kHTC - 1) / kHTC), (unsigned)((s.mh + kHTR - 1) / kHTR), (unsigned)planes);
+  hipLaunchKernelGGL(heat_hpass_nms, gh, dim3(256), 0, st, b.tmp, s.mh, s.mw, b.gauss_w, s.radius, s.peak_thresh,
+                     b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
+  OP_AFTER_LAUNCH("heat_hpass_nms", st);
+  hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,
+                     b.peak_cnt, b.peak_xy, b.peak_score);
+  OP_AFTER_LAUNCH("peak_sort", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
 
+// ---------------- launchers ----------------
+static inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
 static int check_shape(const PostShape& s, const PostBuffers& b) {
-  if (s.mw > 0xffff || s.mh > 0x7fff || s.n_integ > 16 || s.n_integ < 2 || b.maxp > 2048 || s.radius > 32) {
+  if (s.mw > 0xffff || s.mh > 0x7fff || s.n_integ > 16 || s.n_integ < 2 || b.maxp > 2048 || s.radius > kMaxR ||
+      s.mh <= s.radius || s.mw <= s.radius || (int64_t)s.mh * s.mw >= 0x7fffffff) {
     set_error("post-process shape outside kernel limits");
     return OP_ERR_INVALID;
   }
@@ -575,13 +629,20 @@ static int check_shape(const PostShape& s, const PostBuffers& b) {
 int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
   int rc = check_shape(s, b);
   if (rc) return rc;
-  const int64_t total = (int64_t)s.n * OP_N_JOINTS * s.mh * s.mw;
-  hipLaunchKernelGGL(upsample_heat, dim3(nblk(total)), dim3(256), 0, st, src, s, b.up);
-  if ((rc = run_gauss_nms(b.up, s, b, st))) return rc;
+  HeatLow hs;
+  hs.src = src;
+  hs.lh = s.lh;
+  hs.lw = s.lw;
+  hs.mh = s.mh;
+  hs.mw = s.mw;
+  if ((rc = run_heat_tiled(hs, s, b, st))) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
   hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, src, s, b);
+  OP_AFTER_LAUNCH("limb_pairs_low", st);
   hipLaunchKernelGGL(limb_greedy, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
+  OP_AFTER_LAUNCH("limb_greedy", st);
   hipLaunchKernelGGL(grouping, dim3(s.n), dim3(64), 0, st, s, b);
+  OP_AFTER_LAUNCH("grouping", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -593,7 +654,11 @@ int launch_peaks_from_full(const float* heat_full, int32_t n_joint, int32_t mh, 
   (void)mw;
   int rc = check_shape(s, b);
   if (rc) return rc;
-  return run_gauss_nms(heat_full, s, b, st);
+  HeatFull hs;
+  hs.p = heat_full;
+  hs.mh = s.mh;
+  hs.mw = s.mw;
+  return run_heat_tiled(hs, s, b, st);
 }
 
 int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const PostShape& s, PostBuffers& b,
@@ -604,7 +669,9 @@ int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const
   if (rc) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
   hipLaunchKernelGGL(limb_pairs_full, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, paf_full, s, b);
+  OP_AFTER_LAUNCH("limb_pairs_full", st);
   hipLaunchKernelGGL(limb_greedy, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
+  OP_AFTER_LAUNCH("limb_greedy", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -613,6 +680,7 @@ int launch_grouping(const PostShape& s, PostBuffers& b, hipStream_t st) {
   int rc = check_shape(s, b);
   if (rc) return rc;
   hipLaunchKernelGGL(grouping, dim3(s.n), dim3(64), 0, st, s, b);
+  OP_AFTER_LAUNCH("grouping", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -620,6 +688,7 @@ int launch_grouping(const PostShape& s, PostBuffers& b, hipStream_t st) {
 int launch_resize_images(const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y,
                          hipStream_t st) {
   hipLaunchKernelGGL(resize_planar, dim3(nblk((int64_t)c * oh * ow)), dim3(256), 0, st, x, c, h, w, oh, ow, y);
+  OP_AFTER_LAUNCH("resize_planar", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }

@@ -8,6 +8,8 @@
 //   * F.concat((paf, heat, feature)) is a single 192-channel buffer whose slices the producing
 //     convs write directly (no concat copy).
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -19,6 +21,70 @@ namespace op {
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
+
+// ---- debugging aid: guard bands (OP_GUARD=<bytes>) ----
+// Every device buffer gets a band of 0xA5 bytes after it; guard_check() (after each debug-synced
+// launch and at every synchronising entry point) reports the first band a kernel wrote into.
+size_t g_guard = 0;
+struct GuardBand {
+  const char* name;
+  const char* p;
+};
+static std::vector<GuardBand> g_bands;
+static std::mutex g_band_mu;
+
+static void guard_add(const char* name, void* p, hipStream_t st) {
+  if (!g_guard) return;
+  hipMemsetAsync(p, 0xA5, g_guard, st);
+  std::lock_guard<std::mutex> lk(g_band_mu);
+  g_bands.push_back({name, (const char*)p});
+}
+
+static void guard_forget(const void* base, size_t bytes) {
+  if (!g_guard || !base) return;
+  std::lock_guard<std::mutex> lk(g_band_mu);
+  const char* b = (const char*)base;
+  std::vector<GuardBand> keep;
+  for (auto& g : g_bands)
+    if (!(g.p >= b && g.p < b + bytes)) keep.push_back(g);
+  g_bands.swap(keep);
+}
+
+static int guard_check(const char* where) {
+  if (!g_guard) return OP_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipDeviceSynchronize() != hipSuccess) return OP_OK;  // the caller reports the fault itself
+  std::lock_guard<std::mutex> lk(g_band_mu);
+  std::vector<unsigned char> h(g_guard);
+  for (auto& g : g_bands) {
+    if (hipMemcpy(h.data(), g.p, g_guard, hipMemcpyDeviceToHost) != hipSuccess) continue;
+    for (size_t i = 0; i < g_guard; ++i)
+      if (h[i] != 0xA5) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "guard band after buffer '%s' overwritten at +%zu (byte 0x%02x), seen after %s",
+                 g.name, i, h[i], where);
+        fprintf(stderr, "[openpose_hip] %s\n", msg);
+        set_error(msg);
+        (void)cs;
+        return OP_ERR_STATE;
+      }
+  }
+  return OP_OK;
+}
+
+bool g_debug_sync = false;
+int debug_after_launch(const char* name, hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return OP_OK;
+  const hipError_t e1 = hipGetLastError();
+  const hipError_t e2 = hipStreamSynchronize(st);
+  if (e1 != hipSuccess || e2 != hipSuccess) {
+    set_error(std::string("after kernel ") + name + ": " + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    fprintf(stderr, "[openpose_hip] fault after kernel %s: %s\n", name, hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    return OP_ERR_HIP;
+  }
+  return guard_check(name);
+}
 
 struct LayerDef {
   const char* name;
@@ -144,9 +210,10 @@ static void pack_split_into(std::vector<uint16_t>& dst, int cop, int cin16, int 
         const float v = W[(((size_t)co * Ci + ci) * k + ky) * k + kx];
         const uint16_t hb = bf16_rne(v);
         const uint16_t lb = bf16_rne(v - bf16_f(hb));
-        const size_t base = ((((size_t)c16 * taps + t) * cop + (co_off + co)) * 2 + h) * 16;
-        dst[base + j] = hb;
-        dst[base + 8 + j] = lb;
+        // planar: [c16][tap][plane = 2h + (0 hi | 1 lo)][cop][8]
+        const size_t tile = ((size_t)c16 * taps + t) * 4;
+        dst[((tile + 2 * h) * cop + (co_off + co)) * 8 + j] = hb;
+        dst[((tile + 2 * h + 1) * cop + (co_off + co)) * 8 + j] = lb;
       }
     }
 }
@@ -235,6 +302,9 @@ struct op_ctx {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   uintptr_t g_key[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // pinned host staging for batched result fetches
+  char* host_stage = nullptr;
+  size_t host_stage_bytes = 0;
 };
 
 namespace op {
@@ -260,11 +330,14 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
       out[i] = a;
       out[i].p = nullptr;
     }
-    total += (fl + 63) / 64 * 64;  // 256-B alignment
+    total += (fl + 63) / 64 * 64 + g_guard / 4;  // 256-B alignment (+ debug guard band)
   }
   (void)c;
   return total;
 }
+
+static const char* const kBufName[B_COUNT] = {"X0",  "C11", "C12", "P1",  "C21", "C22", "P2",  "C3A", "C3B", "C34",
+                                              "P3",  "C41", "C42", "C43", "CAT", "BRA", "BRB", "S1",  "MAP32"};
 
 static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   if (h % 8 || w % 8 || h < 16 || w < 16 || n < 1) {
@@ -275,20 +348,27 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   Act a[B_COUNT];
   const size_t need = geom_floats(c, n, h, w, a, c->split) * sizeof(float);
   if (need > c->arena_bytes) {
-    if (c->arena) OP_HIP_CHECK(hipFree(c->arena));
+    if (c->arena) {
+      OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      guard_forget(c->arena, c->arena_bytes);
+      OP_HIP_CHECK(hipFree(c->arena));
+    }
     c->arena = nullptr;
     OP_HIP_CHECK(hipMalloc(&c->arena, need));
     c->arena_bytes = need;
   }
+  guard_forget(c->arena, c->arena_bytes);
+  // zero halos (and everything else) once per geometry; kernels only ever write interiors
+  OP_HIP_CHECK(hipMemsetAsync(c->arena, 0, need, c->stream));
   float* p = (float*)c->arena;
   for (int i = 0; i < B_COUNT; ++i) {
     a[i].p = p;
     const size_t fl = a[i].frame_floats() * (size_t)n;
     p += (fl + 63) / 64 * 64;
+    guard_add(kBufName[i], p, c->stream);
+    p += g_guard / 4;
     c->buf[i] = a[i];
   }
-  // zero halos (and everything else) once per geometry; kernels only ever write interiors
-  OP_HIP_CHECK(hipMemsetAsync(c->arena, 0, need, c->stream));
   c->gn = n;
   c->gh = h;
   c->gw = w;
@@ -316,6 +396,8 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
       {(void**)&b.peak_xy, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
       {(void**)&b.peak_score, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
       {(void**)&b.peak_cnt, (size_t)nn * OP_N_JOINTS * 4},
+      {(void**)&b.stage_key, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
+      {(void**)&b.stage_score, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
       {(void**)&b.cand_score, (size_t)nn * OP_N_LIMBS * b.maxc * 8},
       {(void**)&b.cand_idx, (size_t)nn * OP_N_LIMBS * b.maxc * 4},
       {(void**)&b.cand_cnt, (size_t)nn * OP_N_LIMBS * 4},
@@ -330,19 +412,30 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
       {(void**)&b.res_hdr, (size_t)nn * 4 * 4},
       {(void**)&b.gauss_w, 64 * 8},
   };
+  static const char* const part_name[] = {"up",       "tmp",       "hm",        "peak_xy",    "peak_score",
+                                          "peak_cnt", "stage_key", "stage_score", "cand_score", "cand_idx",
+                                          "cand_cnt", "conn_ab",   "conn_score", "conn_cnt",   "sub_ids",
+                                          "sub_sc",   "res_poses", "res_scores", "res_subsets", "res_hdr",
+                                          "gauss_w"};
   size_t total = 0;
-  for (auto& q : parts) total += (q.bytes + 255) / 256 * 256;
+  for (auto& q : parts) total += (q.bytes + 255) / 256 * 256 + g_guard;
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-  if (c->post_arena) OP_HIP_CHECK(hipFree(c->post_arena));
+  if (c->post_arena) {
+    guard_forget(c->post_arena, c->post_bytes);
+    OP_HIP_CHECK(hipFree(c->post_arena));
+  }
   c->post_arena = nullptr;
   OP_HIP_CHECK(hipMalloc(&c->post_arena, total));
   c->post_bytes = total;
-  char* p = (char*)c->post_arena;
-  for (auto& q : parts) {
-    *q.p = p;
-    p += (q.bytes + 255) / 256 * 256;
-  }
   OP_HIP_CHECK(hipMemset(c->post_arena, 0, total));
+  char* p = (char*)c->post_arena;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    *parts[i].p = p;
+    p += (parts[i].bytes + 255) / 256 * 256;
+    guard_add(part_name[i], p, nullptr);
+    p += g_guard;
+  }
+  OP_HIP_CHECK(hipDeviceSynchronize());
   OP_HIP_CHECK(hipMemcpy(b.gauss_w, c->gauss_host.data(), c->gauss_host.size() * 8, hipMemcpyHostToDevice));
   c->pb = b;
   c->pn = nn;
@@ -355,14 +448,24 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
   return OP_OK;
 }
 
-static int ensure_scratch(op_ctx* c, size_t bytes) {
-  if (bytes <= c->scratch_bytes) return OP_OK;
+// (Re)allocate a growable device buffer of `bytes` (+ debug guard band after it).
+static int grow_buffer(op_ctx* c, void** p, size_t* cap, size_t bytes, const char* name) {
+  if (bytes <= *cap) return OP_OK;
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-  if (c->d_scratch) OP_HIP_CHECK(hipFree(c->d_scratch));
-  c->d_scratch = nullptr;
-  OP_HIP_CHECK(hipMalloc(&c->d_scratch, bytes));
-  c->scratch_bytes = bytes;
+  if (*p) {
+    guard_forget(*p, *cap + g_guard);
+    OP_HIP_CHECK(hipFree(*p));
+  }
+  *p = nullptr;
+  OP_HIP_CHECK(hipMalloc(p, bytes + g_guard));
+  *cap = bytes;
+  guard_add(name, (char*)*p + bytes, nullptr);
+  OP_HIP_CHECK(hipDeviceSynchronize());
   return OP_OK;
+}
+
+static int ensure_scratch(op_ctx* c, size_t bytes) {
+  return grow_buffer(c, (void**)&c->d_scratch, &c->scratch_bytes, bytes, "scratch");
 }
 
 // ---- forward plan ----
@@ -439,6 +542,8 @@ static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_
   return g;
 }
 
+static int g_halo_mode = 1;  // OP_HALO_MODE env: 0 gather, 1 halo x1 buffer, 2 halo x2 buffers
+
 static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups) {
   SplitConvShape s;
   s.n = n;
@@ -453,6 +558,7 @@ static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks
   s.relu = relu ? 1 : 0;
   s.groups = groups;
   s.cs_out32 = 0;
+  s.halo_mode = g_halo_mode;
   return s;
 }
 
@@ -743,6 +849,9 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
     return OP_ERR_HIP;
   }
   for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
+  if (const char* e = getenv("OP_HALO_MODE")) op::g_halo_mode = atoi(e);
+  if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
+  if (const char* e = getenv("OP_GUARD")) op::g_guard = ((size_t)atol(e) + 255) / 256 * 256;
   // scipy _gaussian_kernel1d(sigma, 0, int(4*sigma + 0.5)) taps (restated; pinned by the tests)
   {
     const double sigma = c->prm.gaussian_sigma;
@@ -803,11 +912,17 @@ int op_destroy(op_ctx* c) {
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
   free_weights(c);
+  guard_forget(c->arena, c->arena_bytes);
+  guard_forget(c->post_arena, c->post_bytes);
+  guard_forget(c->d_frames, c->frames_bytes + g_guard);
+  guard_forget(c->d_maps, c->maps_bytes + g_guard);
+  guard_forget(c->d_scratch, c->scratch_bytes + g_guard);
   if (c->arena) hipFree(c->arena);
   if (c->post_arena) hipFree(c->post_arena);
   if (c->d_frames) hipFree(c->d_frames);
   if (c->d_maps) hipFree(c->d_maps);
   if (c->d_scratch) hipFree(c->d_scratch);
+  if (c->host_stage) hipHostFree(c->host_stage);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
@@ -1123,7 +1238,7 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
   OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_ab, ab.data(), ab.size() * 4, hipMemcpyHostToDevice, c->stream));
   OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_score, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, c->stream));
   PostShape s;
-  post_shape(c, s, 1, 8, 8, 8, 8, 8.0, 1.0, 1.0);
+  post_shape(c, s, 1, 64, 64, 64, 64, 64.0, 1.0, 1.0);  // map size is unused by grouping
   RC(launch_grouping(s, c->pb, c->stream));
   int32_t hdr[4];
   OP_HIP_CHECK(hipMemcpyAsync(hdr, c->pb.res_hdr, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
@@ -1156,13 +1271,7 @@ static int stage_maps_dev(op_ctx* c, const float* maps, int n, int lh, int lw, f
       for (int y = 0; y < lh; ++y)
         for (int x = 0; x < lw; ++x)
           t[(((size_t)f * lh + y) * lw + x) * 57 + ch] = maps[(((size_t)f * 57 + ch) * lh + y) * lw + x];
-  if (fl * 4 > c->maps_bytes) {
-    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (c->d_maps) OP_HIP_CHECK(hipFree(c->d_maps));
-    c->d_maps = nullptr;
-    OP_HIP_CHECK(hipMalloc(&c->d_maps, fl * 4));
-    c->maps_bytes = fl * 4;
-  }
+  RC(grow_buffer(c, (void**)&c->d_maps, &c->maps_bytes, fl * 4, "maps"));
   OP_HIP_CHECK(hipMemcpy(c->d_maps, t.data(), fl * 4, hipMemcpyHostToDevice));
   *out = c->d_maps;
   return OP_OK;
@@ -1247,13 +1356,7 @@ int op_stage_frames(op_ctx* c, const uint8_t* frames, int32_t n, int32_t h, int3
     return OP_ERR_INVALID;
   }
   const size_t bytes = (size_t)n * h * w * 3;
-  if (bytes > c->frames_bytes) {
-    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (c->d_frames) OP_HIP_CHECK(hipFree(c->d_frames));
-    c->d_frames = nullptr;
-    OP_HIP_CHECK(hipMalloc(&c->d_frames, bytes));
-    c->frames_bytes = bytes;
-  }
+  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpyAsync(c->d_frames, frames, bytes, hipMemcpyHostToDevice, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   if (c->st_n != n || c->st_h != h || c->st_w != w) {
@@ -1349,7 +1452,13 @@ int op_run_staged_graph(op_ctx* c) {
     OP_HIP_CHECK(e);
     c->graph = g;
     OP_HIP_CHECK(hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
+    if (const char* d = getenv("OP_GRAPH_DUMP")) {  // debugging aid: DOT dump of every captured graph
+      static int seq = 0;
+      const std::string path = std::string(d) + "/graph_" + std::to_string(seq++) + ".dot";
+      hipGraphDebugDotPrint(g, path.c_str(), hipGraphDebugDotFlagsVerbose);
+    }
   }
+  if (getenv("OP_GRAPH_DRYRUN")) return enqueue_staged(c, false);  // debugging aid: eager instead of replay
   OP_HIP_CHECK(hipGraphLaunch(c->gexec, c->stream));
   c->timed = false;
   return OP_OK;
@@ -1359,6 +1468,7 @@ int op_synchronize(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, false));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  RC(guard_check("op_synchronize"));
   return OP_OK;
 }
 
@@ -1380,6 +1490,62 @@ int op_fetch_result(op_ctx* c, int32_t frame, double* poses, double* scores, int
   return read_result(c, frame, poses, scores, cap, res);
 }
 
+int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double* scores, int32_t cap,
+                     op_frame_result* res) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!res || !poses || !scores || first < 0 || n < 1 || first + n > c->st_n || cap < 1) {
+    set_error("op_fetch_results: bad range");
+    return OP_ERR_INVALID;
+  }
+  std::vector<int32_t> hdr((size_t)n * 4);
+  OP_HIP_CHECK(hipMemcpy(hdr.data(), c->pb.res_hdr + 4 * first, hdr.size() * 4, hipMemcpyDeviceToHost));
+  int in_w, in_h, map_w, map_h;
+  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
+  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  int maxp = 0;
+  for (int i = 0; i < n; ++i) {
+    op_frame_result& r = res[i];
+    memset(&r, 0, sizeof(r));
+    r.status = hdr[4 * i];
+    r.n_peaks = hdr[4 * i + 1];
+    r.n_persons = r.status == OP_OK ? hdr[4 * i + 2] : 0;
+    r.map_w = map_w;
+    r.map_h = map_h;
+    r.net_w = in_w;
+    r.net_h = in_h;
+    maxp = std::max(maxp, r.n_persons);
+  }
+  if (maxp > cap) {
+    set_error("result capacity too small");
+    return OP_ERR_CAPACITY;
+  }
+  if (maxp > 0) {
+    // strided device rows -> packed pinned staging (one async 2D copy each), then host rows
+    const size_t prow = (size_t)maxp * 54 * 8, srow = (size_t)maxp * 8;
+    const size_t need = (size_t)n * (prow + srow);
+    if (need > c->host_stage_bytes) {
+      if (c->host_stage) OP_HIP_CHECK(hipHostFree(c->host_stage));
+      c->host_stage = nullptr;
+      OP_HIP_CHECK(hipHostMalloc((void**)&c->host_stage, need, hipHostMallocDefault));
+      c->host_stage_bytes = need;
+    }
+    char* hp = c->host_stage;
+    char* hs = c->host_stage + (size_t)n * prow;
+    OP_HIP_CHECK(hipMemcpy2DAsync(hp, prow, c->pb.res_poses + (size_t)first * c->pb.maxs * 54,
+                                  (size_t)c->pb.maxs * 54 * 8, prow, n, hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipMemcpy2DAsync(hs, srow, c->pb.res_scores + (size_t)first * c->pb.maxs, (size_t)c->pb.maxs * 8,
+                                  srow, n, hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+      const size_t k = (size_t)res[i].n_persons;
+      memcpy((char*)poses + (size_t)i * cap * 54 * 8, hp + i * prow, k * 54 * 8);
+      memcpy((char*)scores + (size_t)i * cap * 8, hs + i * srow, k * 8);
+    }
+  }
+  return OP_OK;
+}
+
 int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, double* poses, double* scores,
               int32_t cap, op_frame_result* res) {
   using namespace op;
@@ -1389,13 +1555,7 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
     return OP_ERR_INVALID;
   }
   const size_t bytes = (size_t)h * w * 3;
-  if (bytes > c->frames_bytes) {
-    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-    if (c->d_frames) OP_HIP_CHECK(hipFree(c->d_frames));
-    c->d_frames = nullptr;
-    OP_HIP_CHECK(hipMalloc(&c->d_frames, bytes));
-    c->frames_bytes = bytes;
-  }
+  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
                                 hipMemcpyHostToDevice, c->stream));
   c->st_n = 1;
@@ -1407,6 +1567,7 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
   c->use_maps = keep_maps;
   if (rc) return rc;
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  RC(guard_check("op_detect"));
   return op_fetch_result(c, 0, poses, scores, cap, res);
 }
 

@@ -152,6 +152,12 @@ int op_synchronize(op_ctx* ctx);
 /* Results of staged frame i (after op_synchronize). */
 int op_fetch_result(op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap, op_frame_result* res);
 
+/* Results of staged frames [first, first+n) in three copies: poses (n x cap x 18 x 3 f64),
+ * scores (n x cap f64), res (n headers).  A frame's status is in its header; the call itself
+ * fails only on bad arguments / HIP errors or when a frame's person count exceeds cap. */
+int op_fetch_results(op_ctx* ctx, int32_t first, int32_t n, double* poses, double* scores, int32_t cap,
+                     op_frame_result* res);
+
 /* HIP-event timing of the last op_run_staged: ms spent in the conv kernels, the post-process kernels
  * and total, recorded on the context stream. */
 int op_last_timing(op_ctx* ctx, double* conv_ms, double* post_ms, double* total_ms);

@@ -143,6 +143,9 @@ def test_staged_batch_matches_single_and_graph(ctx, prec):
             p, s, r = ctx.fetch_result(i)
             assert r.n_peaks == single[i][2].n_peaks
             assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
+        for i, (p, s, r) in enumerate(ctx.fetch_results(0, 3, cap=2048)):
+            assert r.n_peaks == single[i][2].n_peaks and r.status == 0
+            assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
     ctx.set_precision("bf16x3")
 
 
