@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libopenpose_hip.so")
+# OP_LIB_VARIANT=<name> loads libopenpose_hip.<name>.so instead (kernel tuning experiments only)
+LIB_PATH = os.path.join(_HERE, "libopenpose_hip%s.so" % (
+    "." + os.environ["OP_LIB_VARIANT"] if os.environ.get("OP_LIB_VARIANT") else ""))
 
 OP_OK, OP_ERR_INVALID, OP_ERR_HIP, OP_ERR_CAPACITY, OP_ERR_INDEX, OP_ERR_STATE = range(6)
 N_JOINTS, N_LIMBS, N_PAF, N_HEAT, N_LAYERS = 18, 19, 38, 19, 92

@@ -1,0 +1,394 @@
+// Halo-tiled convolution with weights shared across the workgroup (3xBF16 split, gfx950): the
+// 7x7 stage convs (Mconv1..5 of stages 2-6, 68 % of the network's FLOPs) and the 3x3 convs.
+//
+// Workgroup = NWAVE waves; it owns CW output channels (128 or 64) x one TR x TC pixel tile of one
+// frame.  Wave w holds 64 channels (channel half w / PG) for NPB 32-pixel blocks (pixel group
+// w % PG): 2 x NPB accumulator tiles, so every B fragment read from LDS feeds 2 channel blocks and
+// every A fragment NPB pixel blocks.
+//  * Activations: per 16-channel chunk the tile's input rows plus halo are copied once into LDS
+//    as 4 planes (hi/lo x k-half) of 16 B per pixel and all KSxKS taps read their shifted window
+//    from there.  The LDS row pitch is TC + 16 slots, so a 32-pixel block that wraps a tile row
+//    keeps every ds_read_b128 lane group on distinct banks.
+//  * Weights: (tap, chunk) tiles of CW channels x 4 planes stream through an LDS ring by
+//    global_load_lds (each wave copies its pieces), one counted vmcnt + one s_barrier per tap
+//    (PAIR = 0, 3-deep ring) or per pair of taps (PAIR = 1, 6-deep ring, 4 taps ahead).
+//  * The weight bytes fetched per MFMA-flop fall with the tile's pixel count: 7x7 uses one
+//    8-wave workgroup per CU on 768-pixel tiles; 3x3 uses two 4-wave workgroups per CU on
+//    384-pixel tiles so one workgroup's halo reload (every 9 taps) overlaps the other's MFMAs.
+//  * Workgroup -> XCD: blocks are dealt to XCDs round-robin, so block b is remapped to make every
+//    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
+//  * MFMA: v_mfma_f32_32x32x16_bf16, products hi*hi + hi*lo + lo*hi into one f32 accumulator.
+#include <cstdlib>
+
+#include "common.hpp"
+
+namespace op {
+
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4g __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR_G(p) ((__attribute__((address_space(3))) void*)(p))
+
+struct BigTiling {
+  int32_t tr, tc;            // tile rows x cols
+  int32_t tiles_y, tiles_x;  // tiles per frame
+  int32_t pitch;             // LDS halo row pitch in 16-B slots: >= tc + ks - 1, (pitch - tc) % 16 == 0
+  int32_t hrows;             // tr + ks - 1
+  int32_t nh;                // 1-KiB halo pieces per plane
+  int32_t units;             // weight sets = groups x channel tiles
+  int32_t co_tiles;          // channel tiles per group
+  int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
+  int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 4, "vmcnt literal");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+}
+
+// nt (1 or 2) consecutive taps t, t+1 of one chunk for one wave: 2 channel blocks x NPB pixel
+// blocks.  The B fragments are software-pipelined one block ahead (also into the next tap), so
+// each LDS read has a block's 6 MFMAs (~200 cycles) to land; A fragments are read per tap.
+template <int NPB, int KS, int PLANE_W>
+__device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const char* bp0, int hplane,
+                                         const uint32_t (&qp)[(NPB + 1) / 2], const char* wb0, const char* wb1,
+                                         int t, int pitch, int hi) {
+  bf16x8g bh[2], bl[2], ah[2], al[2];
+  // halo slot of pixel block pb (two 16-bit slots per register)
+  auto q0 = [&](int pb) -> int { return (int)((qp[pb >> 1] >> (16 * (pb & 1))) & 0xffffu); };
+  int toff = (t / KS) * pitch + (t - (t / KS) * KS);
+  bh[0] = *(const bf16x8g*)(bp0 + (q0(0) + toff) * 16);
+  bl[0] = *(const bf16x8g*)(bp0 + hplane + (q0(0) + toff) * 16);
+#pragma unroll 1
+  for (int u = 0; u < nt; ++u) {
+    const char* wb = u == 0 ? wb0 : wb1;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      ah[cb] = *(const bf16x8g*)(wb + (2 * hi) * PLANE_W + cb * 512);
+      al[cb] = *(const bf16x8g*)(wb + (2 * hi + 1) * PLANE_W + cb * 512);
+    }
+    const int tn = t + u + 1;
+    const int toff_n = (tn / KS) * pitch + (tn - (tn / KS) * KS);
+    const bool more = u + 1 < nt;
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      // block pb's fragments sit in buffer (pb & 1) of this tap; an odd NPB flips the parity of
+      // the next tap, so the prefetch into the next tap goes to buffer (NPB & 1)
+      const int cur = pb & 1;
+      if (pb + 1 < NPB) {
+        bh[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + (q0(pb + 1) + toff) * 16);
+        bl[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(pb + 1) + toff) * 16);
+      } else if (more) {
+        bh[NPB & 1] = *(const bf16x8g*)(bp0 + (q0(0) + toff_n) * 16);
+        bl[NPB & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(0) + toff_n) * 16);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the next block's reads ahead of this block's MFMAs
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+      }
+    }
+    toff = toff_n;
+    if constexpr (NPB & 1) {  // the next tap starts on buffer 1: swap so block 0 reads buffer 0
+      const bf16x8g th = bh[0], tl = bl[0];
+      bh[0] = bh[1];
+      bl[0] = bl[1];
+      bh[1] = th;
+      bl[1] = tl;
+    }
+  }
+}
+
+template <int KS, int NPB, int NWAVE, int CW, int PAIR>
+__global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
+                                                                                   SplitConvGroup g1, BigTiling tl) {
+  constexpr int KSQ = KS * KS;
+  constexpr int R = KS / 2;
+  constexpr int CH = CW / 64;            // 64-channel halves per tile
+  constexpr int PG = NWAVE / CH;         // pixel groups
+  constexpr int PLANE_W = CW * 16;       // bytes of one weight plane of the tile
+  constexpr int SLOT_W = 4 * PLANE_W;    // one (tap, chunk) weight tile
+  constexpr int NWP = 4 * CH / NWAVE;    // 1-KiB weight pieces per wave per tap
+  constexpr int RING = PAIR ? 6 : 3;
+  constexpr int AHEAD = PAIR ? 4 : 2;    // taps between a weight copy's issue and its use
+  static_assert(NWP >= 1 && NWP <= 2 && PG >= 1, "wave / channel split");
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
+
+  // ---- which tile / weight set ----
+  const int lin = blockIdx.x;
+  int unit, widx;
+  if (tl.xpu) {
+    const int xcd = lin & 7, slot = lin >> 3;
+    unit = xcd / tl.xpu;
+    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
+  } else {
+    unit = lin / tl.per_unit;
+    widx = lin - unit * tl.per_unit;
+  }
+  if (unit >= tl.units || widx >= tl.per_unit) return;
+  const int grp = unit / tl.co_tiles;
+  const int co0 = (unit - grp * tl.co_tiles) * CW;
+  const SplitConvGroup g = grp == 0 ? g0 : g1;
+  if (co0 >= g.cop) return;  // narrower second group
+  const int tpf = tl.tiles_y * tl.tiles_x;
+  const int frame = widx / tpf;
+  const int tix = widx - frame * tpf;
+  const int ty = tix / tl.tiles_x;
+  const int y0 = ty * tl.tr, x0 = (tix - ty * tl.tiles_x) * tl.tc;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ch = wave / PG;  // channel half: channels co0 + 64*ch .. +63
+  const int pg = wave % PG;  // pixel group: tile pixels pg*NPB*32 .. +NPB*32-1
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int hplane = tl.nh * 1024;
+  char* const halo = lds + RING * SLOT_W;
+  const int wp_in = s.w + 2 * s.pin;
+  const int hp_in = s.h + 2 * s.pin;
+  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
+  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
+
+  // weights: wave w copies pieces j = w*NWP + i: plane j / CH, channels co0 + 64*(j % CH) + 0..63
+  const int64_t wplane = (int64_t)g.cop * 16;
+  const int64_t wstep = 4 * wplane;
+  const char* wsrc[NWP];
+  int wdst[NWP];
+#pragma unroll
+  for (int i = 0; i < NWP; ++i) {
+    const int j = wave * NWP + i;
+    wsrc[i] = (const char*)g.w + (j / CH) * wplane + ((int64_t)co0 + 64 * (j % CH) + lane) * 16;
+    wdst[i] = (j / CH) * PLANE_W + (j % CH) * 1024;
+  }
+  const int n_it = s.c16 * KSQ;
+  auto stage_w = [&](int it) {
+    char* dst = lds + (it % RING) * SLOT_W;  // slot of the unclamped step
+    if (it >= n_it) it = n_it - 1;           // trailing copies: never read
+#pragma unroll
+    for (int i = 0; i < NWP; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (int64_t)it * wstep), LDS_PTR_G(dst + wdst[i]), 16,
+                                       0, 0);
+  };
+
+  // this lane's output pixels: tile-local p = (pg*NPB + pb)*32 + l32 -> (r, c) -> halo slot
+  const int rows_here = min(tl.tr, s.h - y0);
+  const int cols_here = min(tl.tc, s.w - x0);
+  uint32_t qp[(NPB + 1) / 2];  // two 16-bit halo slots per register (hrows*pitch <= 4*nh*64 < 65536)
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const int p = (pg * NPB + pb) * 32 + l32;
+    const int r = p / tl.tc, c = p - (p / tl.tc) * tl.tc;
+    const uint32_t q = (r < rows_here && c < cols_here) ? (uint32_t)(r * tl.pitch + c) : 0u;  // pad lanes: never stored
+    if (pb & 1) qp[pb >> 1] |= q << 16;
+    else qp[pb >> 1] = q;
+  }
+
+  floatx16 acc[2][NPB];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[cb][pb][e] = 0.0f;
+
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i) stage_w(i);
+  const char* const bp0 = halo + (2 * hi) * hplane;  // this lane's k-half: hi plane, lo plane follows
+  const int wlane = (ch * 64 + l32) * 16;
+  int it = 0;
+  for (int c = 0; c < s.c16; ++c) {
+    // ---- halo reload; everyone is past the previous chunk's reads ----
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    {
+      const char* src0 = fbase + c * 64;
+      for (int q = wave; q < 4 * tl.nh; q += NWAVE) {
+        const int plane = q / tl.nh, i = q - (q / tl.nh) * tl.nh;
+        const int sl = i * 64 + lane;
+        const int hr = sl / tl.pitch, hc = sl - (sl / tl.pitch) * tl.pitch;
+        int yy = y0 - R + hr + s.pin, xx = x0 - R + hc + s.pin;
+        // slots past the padded image (bottom / right of a partial tile, pitch gap) only feed
+        // masked outputs or are never read: clamp the source inside this frame
+        yy = yy < hp_in - 1 ? yy : hp_in - 1;
+        xx = xx < wp_in - 1 ? xx : wp_in - 1;
+        __builtin_amdgcn_global_load_lds((const void*)(src0 + plane * 16 + ((int64_t)yy * wp_in + xx) * pix_bytes),
+                                         LDS_PTR_G(halo + plane * hplane + i * 1024), 16, 0, 0);
+      }
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (PAIR) {
+#pragma unroll 1
+      for (int t = 0; t < KSQ; t += 2) {
+        // taps (t, t+1) share one barrier: W(it), W(it+1) landed for this wave (W(it+2), W(it+3)
+        // may be in flight; after a 1-tap tail the count over-waits, which is safe) ...
+        wait_vmcnt<2 * NWP>();
+        // ... and for every wave; every wave is also done with the slots of the previous pair
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage_w(it + 4);
+        stage_w(it + 5);
+        const int nt = t + 1 < KSQ ? 2 : 1;
+        big_taps<NPB, KS, PLANE_W>(nt, acc, bp0, hplane, qp, lds + (it % RING) * SLOT_W + wlane,
+                                   lds + ((it + 1) % RING) * SLOT_W + wlane, t, tl.pitch, hi);
+        it += nt;
+      }
+    } else {
+#pragma unroll 1
+      for (int t = 0; t < KSQ; ++t, ++it) {
+        wait_vmcnt<NWP>();  // W(it) landed for this wave (W(it+1) may be in flight) ...
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; slot (it-1) % 3 is free
+        asm volatile("" ::: "memory");
+        stage_w(it + 2);
+        const char* wb = lds + (it % RING) * SLOT_W + wlane;
+        big_taps<NPB, KS, PLANE_W>(1, acc, bp0, hplane, qp, wb, wb, t, tl.pitch, hi);
+      }
+    }
+  }
+  wait_vmcnt<0>();  // drain the trailing (never read) weight copies
+
+  // ---- epilogue: bias, ReLU, split store (+ dense f32 copy) ----
+  const int wp_out = s.w + 2 * s.pout;
+  const int hp_out = s.h + 2 * s.pout;
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const int p = (pg * NPB + pb) * 32 + l32;
+    const int r = p / tl.tc, cc = p - (p / tl.tc) * tl.tc;
+    if (r >= rows_here || cc >= cols_here) continue;
+    const int y = y0 + r, x = x0 + cc;
+    char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
+    float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = co0 + ch * 64 + cb * 32 + 8 * q + 4 * hi;
+        if (co >= g.cout_store) continue;
+        const floatx4 bv = *(const floatx4*)(g.bias + co);
+        floatx4 v;
+        u16x4g vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float f = acc[cb][pb][4 * q + e] + bv[e];
+          if (s.relu) f = f > 0.0f ? f : 0.0f;
+          v[e] = f;
+          const __bf16 h16 = (__bf16)f;
+          const __bf16 l16 = (__bf16)(f - (float)h16);
+          vh[e] = __builtin_bit_cast(unsigned short, h16);
+          vl[e] = __builtin_bit_cast(unsigned short, l16);
+        }
+        char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+        *(u16x4g*)d = vh;
+        *(u16x4g*)(d + 16) = vl;
+        if (o32) *(floatx4*)(o32 + co) = v;
+      }
+  }
+}
+
+// ---- host side ----
+struct BigConfig {
+  int ks, npb, nwave, cw, pair;
+  int cap() const { return (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
+  int ring_bytes() const { return (pair ? 6 : 3) * 4 * cw * 16; }
+  int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
+};
+
+static int halo_bytes(int tr, int tc, int ks) {
+  const int pitch = tc + (ks > 1 ? 16 * ((ks - 1 + 15) / 16) : 0);
+  return 4 * 1024 * (((tr + ks - 1) * pitch + 63) / 64);
+}
+
+// Pick the tile (tr x tc) that fits LDS and wastes the fewest MFMA lanes; false if none fits.
+static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
+  const int cap = k.cap();
+  const int budget = k.lds_budget() - k.ring_bytes();
+  double best = 0.0;
+  for (int segs = 1; segs <= 16; ++segs) {
+    const int tc = (w + segs - 1) / segs;
+    if (tc > cap || tc < 1) continue;
+    int tr = cap / tc;
+    if (tr > h) tr = h;
+    while (tr >= 1 && halo_bytes(tr, tc, k.ks) > budget) --tr;
+    if (tr < 1) continue;
+    const int tiles_y = (h + tr - 1) / tr;
+    const int trb = (h + tiles_y - 1) / tiles_y;  // even the rows out over the same tile count
+    const double util = (double)h * w / ((double)tiles_y * segs * cap);
+    if (util > best + 1e-9) {
+      best = util;
+      t.tr = trb;
+      t.tc = tc;
+      t.tiles_y = tiles_y;
+      t.tiles_x = (w + tc - 1) / tc;
+    }
+  }
+  if (best <= 0.0) return false;
+  t.pitch = t.tc + (k.ks > 1 ? 16 * ((k.ks - 1 + 15) / 16) : 0);
+  t.hrows = t.tr + k.ks - 1;
+  t.nh = (t.hrows * t.pitch + 63) / 64;
+  t.co_tiles = (cop_max + k.cw - 1) / k.cw;
+  t.units = groups * t.co_tiles;
+  t.per_unit = n * t.tiles_y * t.tiles_x;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  return true;
+}
+
+template <int KS, int NPB, int NWAVE, int CW, int PAIR>
+static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
+  const BigConfig k{KS, NPB, NWAVE, CW, PAIR};
+  const int lds = k.ring_bytes() + 4 * tl.nh * 1024;
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+                                 : (unsigned)(tl.units * tl.per_unit);
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+                     s.groups > 1 ? g[1] : g[0], tl);
+  OP_AFTER_LAUNCH("conv_big_bf16x3", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// The split-path convolution on shared-weight halo tiles (7x7 and 3x3).  *taken = 0 when the
+// shape is outside these kernels (the caller falls back).
+int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
+  *taken = 0;
+  if ((s.ks != 7 && s.ks != 3) || s.cs_in % 16 || s.pin < s.ks / 2) return OP_OK;
+  int cop_max = 0;
+  bool c128 = true;
+  for (int i = 0; i < s.groups; ++i) {
+    if (g[i].cop % 64 || g[i].cin_off % 16) return OP_OK;
+    if (g[i].cop % 128) c128 = false;
+    cop_max = cop_max > g[i].cop ? cop_max : g[i].cop;
+  }
+  static const bool plain_order = getenv("OP_BIG_PLAIN_ORDER") != nullptr;  // tuning aid: no XCD remap
+  BigTiling tl;
+  if (s.ks == 7) {
+    if (!c128) return OP_OK;
+    if (!big_tiling(BigConfig{7, 6, 8, 128, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
+    if (plain_order) tl.xpu = 0;
+    *taken = 1;
+    return launch_big_t<7, 6, 8, 128, 1>(s, g, tl, st);
+  }
+  if (c128) {
+    if (!big_tiling(BigConfig{3, 6, 4, 128, 0}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
+    if (plain_order) tl.xpu = 0;
+    *taken = 1;
+    return launch_big_t<3, 6, 4, 128, 0>(s, g, tl, st);
+  }
+  if (!big_tiling(BigConfig{3, 3, 4, 64, 0}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
+  if (plain_order) tl.xpu = 0;
+  *taken = 1;
+  return launch_big_t<3, 3, 4, 64, 0>(s, g, tl, st);
+}
+
+}  // namespace op
