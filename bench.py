@@ -58,13 +58,40 @@ def cpu_baseline(frames, maps, n_frames):
                       "restatement on the same 6-person maps; %.1f s total" % (n_frames, dt)}
 
 
+KERNEL_7X7 = {0: "conv_bf16x3<7", 1: "conv7_halo_bf16x3", 2: "conv7_halo_bf16x3", 3: "conv_halo_bf16x3<7",
+              4: "conv_big_bf16x3<7", 5: "conv_big_bf16x3<7"}
+
+
+def committed_traffic(kernel, batch, precision, halo_mode):
+    """HBM bytes per launch (read + write) of `kernel` from the newest committed rocprofv3 PMC
+    summary (profiles/*_traffic.json, FETCH_SIZE x2 + WRITE_SIZE, tools/summarize_profile.py) taken
+    on this exact workload; (None, None) when no profile matches."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("config") or {}
+        if cfg.get("frames_per_step_per_gpu") != batch or d.get("precision", "bf16x3") != precision:
+            continue
+        if d.get("halo_mode", 1) != halo_mode:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.replace("op::", "").startswith(kernel):
+                best = (int(v["read_bytes"] + v["write_bytes"]), os.path.basename(p))
+    return best if best else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=28,
-                    help="frames per step per GPU (28 fills 2 workgroups/CU of the 7x7 kernel: 9 tiles x 28 x 2)")
+    ap.add_argument("--batch", type=int, default=42,
+                    help="frames per step per GPU (42: the 7x7 kernel's 3 tiles/frame x 2 branches x 42 = 252 "
+                         "workgroups, one per CU)")
     ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
                     help="post-process input: COCO-like 6-person maps (default) or the random-weight "
                          "network's own last stage")
@@ -90,6 +117,7 @@ def main():
     Fr = importlib.import_module(PKG + ".frames")
 
     B = args.batch
+    halo_mode = int(os.environ.get("OP_HALO_MODE", "4"))
     limits = L.OpLimits()
     limits.max_batch = B
     ctx = L.Context(local, None, limits)
@@ -156,13 +184,15 @@ def main():
         if args.precision == "bf16x3":
             # 3 bf16 MFMA products per f32-accurate MAC: the f32-accurate peak is 2500/3 TFLOP/s
             peak = BF16_DENSE_PEAK_TFLOPS / 3.0
-            kern = "conv_bf16x3<7,4,2> (7x7 stage convs, 3xBF16 split on v_mfma_f32_32x32x16_bf16)"
+            kern = "%s (7x7 stage convs, 3xBF16 split on v_mfma_f32_32x32x16_bf16)" % KERNEL_7X7.get(
+                halo_mode, "conv_bf16x3<7")
         else:
             peak = FP32_MATRIX_PEAK_TFLOPS
             kern = "conv_mfma_f32<7,2,2> (7x7 stage convs, v_mfma_f32_32x32x2_f32)"
+        traffic, tsrc = committed_traffic(kern.split(" ")[0], B, args.precision, halo_mode)
         roofline = {"bound": "mfma", "kernel": kern,
                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
                     "launch_ms": round(ms7 / n7, 4), "flops_per_launch": fl7 / n7,
                     "algorithmic_bytes_per_launch": by7 / n7}
     stage_ms = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}

@@ -542,7 +542,11 @@ static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_
   return g;
 }
 
-static int g_halo_mode = 1;  // OP_HALO_MODE env: 0 gather, 1 halo x1 buffer, 2 halo x2 buffers
+// Split-path conv kernel family (OP_HALO_MODE env, tuning aid): 4 (default) shared-weight halo tiles
+// for 7x7 + 3x3 (conv_big.hip); 5 the same for 7x7 only; 3 co-split halo (conv_halo.hip); 1/2 the
+// 7x7 halo kernel with a single / double halo buffer; 0 the per-tap gather kernel everywhere.
+// Shapes a kernel does not take fall back to the gather kernel.
+static int g_halo_mode = 4;
 
 static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups) {
   SplitConvShape s;

@@ -64,7 +64,9 @@ def main():
             "%.1f" % fr if fr is not None else "-", "%.1f" % wr if wr is not None else "-"))
     os.makedirs(os.path.join(repo, "profiles"), exist_ok=True)
     open(os.path.join(repo, "profiles", tag + ".md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"tag": tag, "config": bench.get("config"), "dtype": bench.get("dtype"), "kernels": traffic},
+    json.dump({"tag": tag, "config": bench.get("config"), "dtype": bench.get("dtype"),
+               "precision": "fp32" if bench.get("dtype") == "f32" else "bf16x3",
+               "halo_mode": int(os.environ.get("OP_HALO_MODE", "4")), "kernels": traffic},
               open(os.path.join(repo, "profiles", tag + "_traffic.json"), "w"), indent=1)
     print("\n".join(lines[:30]))
 
