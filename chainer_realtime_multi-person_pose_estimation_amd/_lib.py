@@ -24,8 +24,9 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
-    "op_set_precision", "op_get_precision", "op_fetch_results",
+    "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
 )
+MAX_SCALES = 8
 PRECISION = {"fp32": 0, "bf16x3": 1}
 
 
@@ -37,7 +38,8 @@ class OpParams(ctypes.Structure):
         ("inner_product_thresh", ctypes.c_double), ("limb_length_ratio", ctypes.c_double),
         ("length_penalty_value", ctypes.c_double), ("n_subset_limbs_thresh", ctypes.c_int32),
         ("subset_score_thresh", ctypes.c_double), ("limbs_point", (ctypes.c_int32 * 2) * N_LIMBS),
-        ("downscale", ctypes.c_int32),
+        ("downscale", ctypes.c_int32), ("n_scales", ctypes.c_int32),
+        ("inference_scales", ctypes.c_double * MAX_SCALES),
     ]
 
 
@@ -74,6 +76,8 @@ def lib():
         "op_destroy": ([P], ctypes.c_int),
         "op_set_weights": ([P, P, P], ctypes.c_int),
         "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
+        "op_detect_precise": ([P, P, I32, I32, I64, P, P, I32, P, P, P], ctypes.c_int),
+        "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
         "op_forward": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
         "op_resize_images": ([P, P, I32, I32, I32, I32, I32, P], ctypes.c_int),
@@ -140,6 +144,13 @@ def params_from_dict(d):
               "length_penalty_value", "subset_score_thresh"):
         if k in d:
             setattr(p, k, float(d[k]))
+    if "inference_scales" in d:
+        sc = list(d["inference_scales"])
+        if not 1 <= len(sc) <= MAX_SCALES:
+            raise ValueError("inference_scales: 1..%d entries" % MAX_SCALES)
+        p.n_scales = len(sc)
+        for i, v in enumerate(sc):
+            p.inference_scales[i] = float(v)
     if "limbs_point" in d:
         for i, (a, b) in enumerate(d["limbs_point"]):
             p.limbs_point[i][0] = int(a)
@@ -225,6 +236,42 @@ class Context(object):
         check(lib().op_detect(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], ptr(poses), ptr(scores),
                               cap, ctypes.byref(res)), "op_detect")
         return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    def detect_precise(self, img, cap=2048, return_maps=False):
+        """detect_precise (pose_detector.py:433-482): (poses, scores, res[, pafs (38,h,w), heatmaps (19,h,w)])."""
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        if img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        h, w = img.shape[:2]
+        poses, scores, res = self._result_arrays(cap)
+        pafs = np.empty((N_PAF, h, w), np.float32) if return_maps else None
+        heat = np.empty((N_HEAT, h, w), np.float32) if return_maps else None
+        rc = lib().op_detect_precise(self.h, ptr(img), h, w, img.strides[0], ptr(poses), ptr(scores), cap,
+                                     ctypes.byref(res), ptr(pafs) if return_maps else None,
+                                     ptr(heat) if return_maps else None)
+        try:
+            check(rc, "op_detect_precise")
+        except IndexError as e:  # the averaged maps are valid: keep them for inspection
+            e.maps = (pafs, heat)
+            raise
+        out = (poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res)
+        return out + (pafs, heat) if return_maps else out
+
+    def resize_cubic(self, img, out_w, out_h):
+        """cv2.resize(img, (out_w, out_h), interpolation=cv2.INTER_CUBIC) for uint8 / float32 H x W (x C)."""
+        a = np.asarray(img)
+        if a.dtype == np.uint8:
+            dt = 0
+        elif a.dtype == np.float32:
+            dt = 1
+        else:
+            raise ValueError("uint8 or float32 image expected")
+        a = np.ascontiguousarray(a)
+        cn = 1 if a.ndim == 2 else a.shape[2]
+        out = np.empty((out_h, out_w, cn), a.dtype)
+        check(lib().op_resize_cubic(self.h, ptr(a), dt, a.shape[0], a.shape[1], cn, ptr(out), out_h, out_w),
+              "op_resize_cubic")
+        return out if a.ndim == 3 else out[:, :, 0]
 
     def preprocess(self, img, out_w, out_h):
         img = np.ascontiguousarray(img, dtype=np.uint8)

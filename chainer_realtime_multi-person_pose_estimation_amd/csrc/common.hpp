@@ -104,6 +104,14 @@ int launch_preprocess(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
 int launch_preprocess_planar(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t dh,
                              int32_t dw, float* out_nchw, hipStream_t st);
 
+// ---- multi-scale path (precise.hip) ----
+int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
+                            int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);
+int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
+                            float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st);
+int launch_resize_cubic_u8(const uint8_t* src, int64_t sstride, int32_t sh, int32_t sw, int32_t cn, uint8_t* dst,
+                           int32_t dh, int32_t dw, hipStream_t st);
+
 // Post-process device state for a batch of frames.
 struct PostBuffers {
   int32_t maxp;        // peaks per joint cap

@@ -1,0 +1,144 @@
+// Kernels of the multi-scale path PoseDetector.detect_precise (pose_detector.py:433-482):
+// cv2.resize(INTER_CUBIC) of the frame fused with pad_image + preprocess into the network input,
+// and the cubic resizes of the last-stage maps (to the padded size, crop, to the original size)
+// fused with the running sum over scales and the final division by the scale count.
+#include "common.hpp"
+#include "cvcubic.hpp"
+
+namespace op {
+
+__device__ __forceinline__ float norm_u8(int v) { return __fsub_rn(__fdiv_rn((float)v, 255.0f), 0.5f); }
+
+// Padded network input (h = ph, w = pw, 1-pixel zero halo): pixel (x, y) < (rw, rh) is the cubic
+// resize of the frame, the rest the pad colour (104, 117, 123) (pose_detector.py:446, :46-55),
+// normalised (x/255 - 0.5, :426-431).  SPLIT: 16 channels as bf16 hi/lo (split format), else
+// 8 f32 channels.
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void preprocess_cubic(const uint8_t* __restrict__ bgr, int64_t row_stride, int sh,
+                                                        int sw, int rh, int rw, int ph, int pw, char* __restrict__ out) {
+  const int wp = pw + 2, hp = ph + 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)hp * wp) return;
+  const int px = (int)(i % wp), py = (int)(i / wp);
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int dx = px - 1, dy = py - 1;
+  if (dx >= 0 && dx < pw && dy >= 0 && dy < ph) {
+    if (dx < rw && dy < rh) {
+      const CubicTap tx = cv_cubic_tap(dx, rw, sw);
+      const CubicTap ty = cv_cubic_tap(dy, rh, sh);
+      const int simd_end = rw * 3 / 8 * 8;
+      for (int ch = 0; ch < 3; ++ch)
+        v[ch] = norm_u8(cv_cubic_u8(bgr, row_stride, sh, sw, 3, ch, tx, ty, dx * 3 + ch, simd_end));
+    } else {
+      v[0] = norm_u8(104);
+      v[1] = norm_u8(117);
+      v[2] = norm_u8(123);
+    }
+  }
+  if constexpr (SPLIT) {
+    unsigned short hs[8], ls[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const __bf16 h16 = (__bf16)v[k];
+      const __bf16 l16 = (__bf16)(v[k] - (float)h16);
+      hs[k] = __builtin_bit_cast(unsigned short, h16);
+      ls[k] = __builtin_bit_cast(unsigned short, l16);
+    }
+    uint4* o = (uint4*)(out + i * 64);
+    o[0] = *(const uint4*)hs;
+    o[1] = *(const uint4*)ls;
+    o[2] = make_uint4(0, 0, 0, 0);
+    o[3] = make_uint4(0, 0, 0, 0);
+  } else {
+    floatx4* o = (floatx4*)(out + i * 32);
+    o[0] = floatx4{v[0], v[1], v[2], v[3]};
+    o[1] = floatx4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
+                            int32_t ph, int32_t pw, bool split, float* out, hipStream_t st) {
+  const int64_t total = (int64_t)(ph + 2) * (pw + 2);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (split)
+    hipLaunchKernelGGL(preprocess_cubic<true>, grid, dim3(256), 0, st, bgr, row_stride, sh, sw, rh, rw, ph, pw,
+                       (char*)out);
+  else
+    hipLaunchKernelGGL(preprocess_cubic<false>, grid, dim3(256), 0, st, bgr, row_stride, sh, sw, rh, rw, ph, pw,
+                       (char*)out);
+  OP_AFTER_LAUNCH("preprocess_cubic", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// Generic cv2.resize(INTER_CUBIC) of a cn-channel f32 image (element (y, x, c) at
+// src[y*sstride + x*pstride + c]) to dh x dw.
+//   mode 0: dst NHWC (dh, dw, cn) contiguous;
+//   mode 1/2/3: dst planar (cn, dh, dw): 1 store, 2 add to dst, 3 add then divide by `div`
+//   (the running sum over scales of pose_detector.py:463/467 and its mean at :469-470).
+__global__ __launch_bounds__(256) void resize_cubic_f32(const float* __restrict__ src, int64_t sstride, int pstride,
+                                                        int sh, int sw, int cn, float* __restrict__ dst, int dh, int dw,
+                                                        int mode, float div) {
+  const int64_t total = (int64_t)cn * dh * dw;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  int x, y, c;
+  if (mode == 0) {
+    c = (int)(i % cn);
+    x = (int)((i / cn) % dw);
+    y = (int)(i / ((int64_t)cn * dw));
+  } else {
+    x = (int)(i % dw);
+    y = (int)((i / dw) % dh);
+    c = (int)(i / ((int64_t)dw * dh));
+  }
+  const CubicTap tx = cv_cubic_tap(x, dw, sw);
+  const CubicTap ty = cv_cubic_tap(y, dh, sh);
+  const float v = cv_cubic_f32(src, sstride, pstride, sh, sw, c, tx, ty, x * cn + c, dw * cn / 4 * 4);
+  if (mode == 0) {
+    dst[i] = v;
+  } else if (mode == 1) {
+    dst[i] = v;
+  } else if (mode == 2) {
+    dst[i] = __fadd_rn(dst[i], v);
+  } else {
+    dst[i] = __fdiv_rn(__fadd_rn(dst[i], v), div);
+  }
+}
+
+int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
+                            float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st) {
+  const int64_t total = (int64_t)cn * dh * dw;
+  hipLaunchKernelGGL(resize_cubic_f32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, sstride, pstride,
+                     sh, sw, cn, dst, dh, dw, mode, div);
+  OP_AFTER_LAUNCH("resize_cubic_f32", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// Generic cv2.resize(INTER_CUBIC) of a cn-channel uint8 image (row stride sstride bytes) to a
+// contiguous dh x dw x cn image (the stage-level ABI op_resize_cubic).
+__global__ __launch_bounds__(256) void resize_cubic_u8(const uint8_t* __restrict__ src, int64_t sstride, int sh, int sw,
+                                                       int cn, uint8_t* __restrict__ dst, int dh, int dw) {
+  const int64_t total = (int64_t)cn * dh * dw;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % cn);
+  const int x = (int)((i / cn) % dw);
+  const int y = (int)(i / ((int64_t)cn * dw));
+  const CubicTap tx = cv_cubic_tap(x, dw, sw);
+  const CubicTap ty = cv_cubic_tap(y, dh, sh);
+  dst[i] = (uint8_t)cv_cubic_u8(src, sstride, sh, sw, cn, c, tx, ty, x * cn + c, dw * cn / 8 * 8);
+}
+
+int launch_resize_cubic_u8(const uint8_t* src, int64_t sstride, int32_t sh, int32_t sw, int32_t cn, uint8_t* dst,
+                           int32_t dh, int32_t dw, hipStream_t st) {
+  const int64_t total = (int64_t)cn * dh * dw;
+  hipLaunchKernelGGL(resize_cubic_u8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, sstride, sh, sw, cn,
+                     dst, dh, dw);
+  OP_AFTER_LAUNCH("resize_cubic_u8", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+}  // namespace op

@@ -302,6 +302,11 @@ struct op_ctx {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   uintptr_t g_key[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // multi-scale path: per-scale map intermediates and the running sums over scales
+  float* d_pmid = nullptr;
+  size_t pmid_bytes = 0;
+  float* d_psum = nullptr;
+  size_t psum_bytes = 0;
   // pinned host staging for batched result fetches
   char* host_stage = nullptr;
   size_t host_stage_bytes = 0;
@@ -775,6 +780,11 @@ int op_default_params(op_params* p) {
                                                {1, 0},  {0, 14},  {0, 15}, {14, 16}, {15, 17}};
   memcpy(p->limbs_point, limbs, sizeof(limbs));
   p->downscale = 8;
+  p->n_scales = 4;
+  p->inference_scales[0] = 0.5;
+  p->inference_scales[1] = 1.0;
+  p->inference_scales[2] = 1.5;
+  p->inference_scales[3] = 2.0;
   return OP_OK;
 }
 
@@ -842,8 +852,10 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
     if (limits->max_frame_h > 0) c->lim.max_frame_h = limits->max_frame_h;
     if (limits->max_frame_w > 0) c->lim.max_frame_w = limits->max_frame_w;
   }
-  if (c->lim.max_peaks_per_joint > 2048 || c->prm.n_integ_points > 16 || c->prm.n_integ_points < 2) {
-    op::set_error("limits outside kernel support (max_peaks_per_joint <= 2048, 2 <= n_integ_points <= 16)");
+  if (c->lim.max_peaks_per_joint > 2048 || c->prm.n_integ_points > 16 || c->prm.n_integ_points < 2 ||
+      c->prm.n_scales < 0 || c->prm.n_scales > OP_MAX_SCALES || c->prm.downscale != 8) {
+    op::set_error("parameters outside kernel support (max_peaks_per_joint <= 2048, 2 <= n_integ_points <= 16, "
+                  "n_scales <= OP_MAX_SCALES, downscale == 8)");
     delete c;
     return OP_ERR_INVALID;
   }
@@ -926,6 +938,10 @@ int op_destroy(op_ctx* c) {
   if (c->d_frames) hipFree(c->d_frames);
   if (c->d_maps) hipFree(c->d_maps);
   if (c->d_scratch) hipFree(c->d_scratch);
+  guard_forget(c->d_pmid, c->pmid_bytes + g_guard);
+  guard_forget(c->d_psum, c->psum_bytes + g_guard);
+  if (c->d_pmid) hipFree(c->d_pmid);
+  if (c->d_psum) hipFree(c->d_psum);
   if (c->host_stage) hipHostFree(c->host_stage);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -1573,6 +1589,125 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   RC(guard_check("op_detect"));
   return op_fetch_result(c, 0, poses, scores, cap, res);
+}
+
+// detect_precise (pose_detector.py:433-482).  Sizes follow the reference's Python arithmetic:
+// multiplier = scale * inference_img_size / min(h, w) and math.ceil(w * multiplier) in f64.
+int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, double* poses,
+                      double* scores, int32_t cap, op_frame_result* res, float* pafs_out, float* heat_out) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (!bgr || !res || h < 11 || w < 11 || row_stride < (int64_t)w * 3 || c->prm.n_scales < 1) {
+    set_error("op_detect_precise: bad arguments (frame >= 11 x 11, at least one inference scale)");
+    return OP_ERR_INVALID;
+  }
+  const size_t bytes = (size_t)h * w * 3;
+  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
+  OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
+                                hipMemcpyHostToDevice, c->stream));
+  c->st_n = 0;  // the staged frame set is replaced
+  const int ds = c->prm.downscale;
+  const int ns = c->prm.n_scales;
+  // per-scale sizes and the largest intermediate
+  int rws[OP_MAX_SCALES], rhs[OP_MAX_SCALES], pws[OP_MAX_SCALES], phs[OP_MAX_SCALES];
+  size_t mid_max = 0;
+  for (int k = 0; k < ns; ++k) {
+    const double m = c->prm.inference_scales[k] * (double)c->prm.inference_img_size / (double)(h < w ? h : w);
+    rws[k] = (int)std::ceil((double)w * m);
+    rhs[k] = (int)std::ceil((double)h * m);
+    pws[k] = rws[k] + (ds - rws[k] % ds) % ds;
+    phs[k] = rhs[k] + (ds - rhs[k] % ds) % ds;
+    if (rws[k] < 1 || rhs[k] < 1 || phs[k] < 16 || pws[k] < 16) {
+      set_error("op_detect_precise: a scale gives a network input below 16 x 16");
+      return OP_ERR_INVALID;
+    }
+    mid_max = std::max(mid_max, (size_t)phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT) * 4);
+  }
+  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_max, "precise_mid"));
+  RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)h * w * (OP_N_PAF + OP_N_HEAT) * 4, "precise_sum"));
+  float* sum_paf = c->d_psum;
+  float* sum_heat = c->d_psum + (size_t)OP_N_PAF * h * w;
+  for (int k = 0; k < ns; ++k) {
+    const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
+    RC(ensure_geometry(c, 1, ph, pw));
+    RC(launch_preprocess_cubic(c->d_frames, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split, c->buf[B_X0].p,
+                               c->stream));
+    RC(run_forward(c));
+    // last-stage maps (lh, lw, cs) with the PAF / heat channels at paf_off / heat_off
+    const int lh = ph / 8, lw = pw / 8;
+    const float* mbase;
+    int64_t mrow;
+    int mpx, paf_off, heat_off;
+    if (c->split) {
+      const Act& m = c->buf[B_MAP32];
+      mbase = m.p;
+      mrow = (int64_t)lw * m.cs;
+      mpx = m.cs;
+      paf_off = 0;
+      heat_off = 40;
+    } else {
+      const Act& cat = c->buf[B_CAT];
+      mrow = (int64_t)(lw + 2 * cat.pad) * cat.cs;
+      mbase = cat.p + cat.pad * mrow + (int64_t)cat.pad * cat.cs;
+      mpx = cat.cs;
+      paf_off = kCatPaf;
+      heat_off = kCatHeat;
+    }
+    // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping)
+    float* mid_paf = c->d_pmid;
+    float* mid_heat = c->d_pmid + (size_t)ph * pw * OP_N_PAF;
+    RC(launch_resize_cubic_f32(mbase + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 0, 1.0f, c->stream));
+    RC(launch_resize_cubic_f32(mbase + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 0, 1.0f, c->stream));
+    // :462-463 / :466-467 crop to rh x rw, cubic to h x w, running sum (mean after the last scale)
+    const int mode = k == 0 ? 1 : (k == ns - 1 ? 3 : 2);
+    RC(launch_resize_cubic_f32(mid_paf, (int64_t)pw * OP_N_PAF, OP_N_PAF, rh, rw, OP_N_PAF, sum_paf, h, w, mode,
+                               (float)ns, c->stream));
+    RC(launch_resize_cubic_f32(mid_heat, (int64_t)pw * OP_N_HEAT, OP_N_HEAT, rh, rw, OP_N_HEAT, sum_heat, h, w, mode,
+                               (float)ns, c->stream));
+  }
+  // :474-482 post-process at the original resolution: img_len = orig_w, no rescale
+  RC(ensure_post(c, 1, h, w));
+  PostShape s;
+  post_shape(c, s, 1, h, w, h, w, (double)w, 1.0, 1.0);
+  RC(launch_peaks_from_full(sum_heat, OP_N_JOINTS, h, w, s, c->pb, c->stream));
+  RC(launch_connections_full(sum_paf, h, w, s, c->pb, c->stream));
+  RC(launch_grouping(s, c->pb, c->stream));
+  if (pafs_out)
+    OP_HIP_CHECK(hipMemcpyAsync(pafs_out, sum_paf, (size_t)OP_N_PAF * h * w * 4, hipMemcpyDeviceToHost, c->stream));
+  if (heat_out)
+    OP_HIP_CHECK(hipMemcpyAsync(heat_out, sum_heat, (size_t)OP_N_HEAT * h * w * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  RC(guard_check("op_detect_precise"));
+  memset(res, 0, sizeof(*res));
+  res->map_w = w;
+  res->map_h = h;
+  res->net_w = pws[ns - 1];
+  res->net_h = phs[ns - 1];
+  return read_result(c, 0, poses, scores, cap, res);
+}
+
+int op_resize_cubic(op_ctx* c, const void* src, int32_t dtype, int32_t h, int32_t w, int32_t cn, void* dst,
+                    int32_t out_h, int32_t out_w) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!src || !dst || (dtype != 0 && dtype != 1) || h < 1 || w < 1 || cn < 1 || out_h < 1 || out_w < 1) {
+    set_error("op_resize_cubic: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const size_t es = dtype == 0 ? 1 : 4;
+  const size_t inb = (size_t)h * w * cn * es, outb = (size_t)out_h * out_w * cn * es;
+  RC(ensure_scratch(c, inb + 256 + outb));
+  char* din = (char*)c->d_scratch;
+  char* dout = din + (inb + 255) / 256 * 256;
+  OP_HIP_CHECK(hipMemcpyAsync(din, src, inb, hipMemcpyHostToDevice, c->stream));
+  if (dtype == 0)
+    RC(launch_resize_cubic_u8((const uint8_t*)din, (int64_t)w * cn, h, w, cn, (uint8_t*)dout, out_h, out_w, c->stream));
+  else
+    RC(launch_resize_cubic_f32((const float*)din, (int64_t)w * cn, cn, h, w, cn, (float*)dout, out_h, out_w, 0, 1.0f,
+                               c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(dst, dout, outb, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
 }
 
 int op_set_precision(op_ctx* c, int32_t mode) {

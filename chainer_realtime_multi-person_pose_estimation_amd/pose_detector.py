@@ -57,11 +57,11 @@ class PoseDetector(object):
         return (np.exp(-0.5 * d2 / sigma ** 2) / (sigma ** 2 * 2 * np.pi)).astype("f")
 
     def pad_image(self, img, stride, pad_value):
-        """pose_detector.py:46-55: pad bottom/right to a multiple of stride with pad_value."""
+        """pose_detector.py:46-55: pad bottom/right to a multiple of stride with pad_value (the
+        reference's result is int64: uint8 zeros plus the pad tuple)."""
         h, w, _ = img.shape
         pad = [(stride - (h % stride)) % stride, (stride - (w % stride)) % stride]
-        out = np.empty((h + pad[0], w + pad[1], 3), "uint8")
-        out[...] = np.asarray(pad_value, dtype=np.int64).astype("uint8")
+        out = np.zeros((h + pad[0], w + pad[1], 3), "uint8") + np.asarray(pad_value)
         out[:h, :w, :] = img
         return out, pad
 
@@ -120,7 +120,19 @@ class PoseDetector(object):
                     raise ValueError("params[%r] differs from the context's; build a new PoseDetector" % k)
 
     def detect_precise(self, orig_img):
-        raise NotImplementedError("precise (multi-scale) inference is not built yet on this path")
+        """pose_detector.py:433-482: multi-scale inference (params['inference_scales'], cubic resizes),
+        post-processed at the original resolution.  Like the reference it leaves the averaged maps in
+        self.pafs (38, H, W) / self.heatmaps (19, H, W) and the peaks in self.all_peaks."""
+        img = np.asarray(orig_img)
+        if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        poses, scores, res, self.pafs, self.heatmaps = self._ctx.detect_precise(img, return_maps=True)
+        self.all_peaks = self.compute_peaks_from_heatmaps(self.heatmaps)
+        if res.n_peaks == 0:
+            return np.empty((0, len(JointType), 3)), np.empty(0)
+        if res.n_persons == 0:
+            return np.array([]), np.empty(0)
+        return poses, scores
 
     def __call__(self, orig_img):
         """pose_detector.py:484-517: BGR uint8 image -> (poses (P,18,3) f64, scores (P,) f64)."""

@@ -33,6 +33,7 @@ extern "C" {
 #define OP_N_PAF 38
 #define OP_N_HEAT 19
 #define OP_N_LAYERS 92 /* models/CocoPoseNet.py:26-129 */
+#define OP_MAX_SCALES 8 /* inference_scales entries (entity.py:74) */
 
 /* Inference parameters — entity.py:70-105 (same names and meaning). */
 typedef struct op_params {
@@ -49,6 +50,8 @@ typedef struct op_params {
   double subset_score_thresh;   /* 0.2 */
   int32_t limbs_point[OP_N_LIMBS][2];
   int32_t downscale;            /* 8 */
+  int32_t n_scales;             /* len(inference_scales) = 4 (detect_precise) */
+  double inference_scales[OP_MAX_SCALES]; /* [0.5, 1, 1.5, 2] */
 } op_params;
 
 /* Capacities of a context (device buffers are sized from these; 0 = default). */
@@ -101,7 +104,24 @@ int op_set_weights(op_ctx* ctx, const float* const* W, const float* const* b);
 int op_detect(op_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride,
               double* poses, double* scores, int32_t cap, op_frame_result* res);
 
+/* PoseDetector.detect_precise (pose_detector.py:433-482), the multi-scale mode (precise=True):
+ * per scale of params.inference_scales a cv2.resize(INTER_CUBIC) of the frame to
+ * ceil(w*m) x ceil(h*m), m = scale * inference_img_size / min(h, w), pad_image to a multiple of
+ * `downscale` with BGR (104, 117, 123), the forward, cubic resizes of the last-stage maps to the
+ * padded size, crop, cubic resize to h x w; the maps are averaged over the scales and
+ * post-processed at the original resolution (img_len = w, no rescale).  pafs_out (38, h, w) and
+ * heat_out (19, h, w) f32 receive the averaged maps (the reference's self.pafs / self.heatmaps)
+ * when non-null. */
+int op_detect_precise(op_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride,
+                      double* poses, double* scores, int32_t cap, op_frame_result* res,
+                      float* pafs_out, float* heat_out);
+
 /* ---- Stage entry points (same semantics as the named reference code; used by the parity tests) ---- */
+
+/* cv2.resize(src, (out_w, out_h), interpolation=cv2.INTER_CUBIC) (pose_detector.py:443, 461-467):
+ * src h x w x cn, dtype 0 = uint8, 1 = float32; dst out_h x out_w x cn of the same dtype. */
+int op_resize_cubic(op_ctx* ctx, const void* src, int32_t dtype, int32_t h, int32_t w, int32_t cn, void* dst,
+                    int32_t out_h, int32_t out_w);
 
 /* cv2.resize(orig_img, (out_w, out_h)) + preprocess (pose_detector.py:493-494, 426-431):
  * x_out (1, 3, out_h, out_w) f32 = u8/255 - 0.5, BGR order kept. */

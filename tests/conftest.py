@@ -37,6 +37,12 @@ def rand_weights():
 
 
 @pytest.fixture(scope="session")
+def rand_weights_small():
+    """Random CocoPoseNet weights scaled for the tiny precise-mode cases (same generator)."""
+    return pkg_module("weights").random_weights(seed=1)
+
+
+@pytest.fixture(scope="session")
 def ctx(lib, rand_weights):
     c = lib.Context(0)
     c.set_weights(rand_weights)

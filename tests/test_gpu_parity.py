@@ -164,3 +164,65 @@ def test_staged_synthetic_maps_match_reference(ctx):
             assert np.array_equal(p.reshape(d["poses"].shape), d["poses"]) and np.array_equal(s, d["scores"])
     finally:
         ctx.use_staged_maps(False)
+
+
+# ---- multi-scale path: detect_precise (pose_detector.py:433-482) ----
+from oracle import precise as PR  # noqa: E402
+
+
+@pytest.mark.parametrize("h,w,oh,ow,cn", [(720, 1280, 184, 328, 3), (50, 70, 37, 91, 3), (17, 23, 61, 45, 1),
+                                          (368, 368, 736, 736, 3)])
+def test_resize_cubic_u8_bit_exact(ctx, h, w, oh, ow, cn):
+    rng = np.random.default_rng(h + w)
+    img = rng.integers(0, 256, (h, w, cn), dtype=np.uint8)
+    assert np.array_equal(ctx.resize_cubic(img, ow, oh), PR.resize_cubic_u8(img, ow, oh))
+
+
+@pytest.mark.parametrize("h,w,oh,ow,cn", [(46, 82, 368, 656, 38), (23, 41, 184, 328, 19), (45, 81, 720, 1280, 19),
+                                          (7, 5, 13, 11, 3)])
+def test_resize_cubic_f32_bit_exact(ctx, h, w, oh, ow, cn):
+    rng = np.random.default_rng(h * w)
+    x = rng.standard_normal((h, w, cn)).astype(np.float32)
+    assert np.array_equal(ctx.resize_cubic(x, ow, oh), PR.resize_cubic_f32(x, ow, oh))
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+def test_detect_precise_vs_oracle(lib, rand_weights_small, prec):
+    params = dict(P.PARAMS, inference_img_size=32)
+    limits = lib.OpLimits()
+    limits.max_peaks_per_joint = 2048
+    c = lib.Context(0, lib.params_from_dict(params), limits)
+    try:
+        c.set_precision(prec)
+        c.set_weights(rand_weights_small)
+        img = np.random.default_rng(5).integers(0, 256, (40, 56, 3), dtype=np.uint8)
+        try:
+            poses, scores, res, pafs, heat = c.detect_precise(img, return_maps=True)
+            raised = False
+        except IndexError as e:  # then the reference raises on these maps too (checked below)
+            pafs, heat = e.maps
+            raised = True
+        want_paf, want_heat = PR.precise_maps(rand_weights_small, img, params)
+        assert pafs.shape == want_paf.shape and heat.shape == want_heat.shape
+        assert np.abs(pafs - want_paf).max() <= FWD_TOL and np.abs(heat - want_heat).max() <= FWD_TOL
+        # the post-process on the GPU's own maps is bit-exact with the oracle's
+        if raised:
+            with pytest.raises(IndexError):
+                PR.postprocess_full(pafs, heat, img.shape[1], params)
+        else:
+            wp, ws = PR.postprocess_full(pafs, heat, img.shape[1], params)
+            assert res.n_peaks == len(P.compute_peaks_from_heatmaps(heat, params))
+            assert np.array_equal(poses.reshape(wp.shape), wp) and np.array_equal(scores, ws)
+    finally:
+        c.close()
+
+
+def test_pose_detector_precise_mode(pkg, rand_weights):
+    det = pkg.PoseDetector("posenet", model=rand_weights, precise=True)
+    img = np.random.default_rng(6).integers(0, 256, (96, 128, 3), dtype=np.uint8)
+    try:
+        poses, scores = det(img)
+    except (IndexError, RuntimeError):
+        return  # random weights: the reference itself may raise / exceed caps on noise maps
+    assert det.pafs.shape == (38, 96, 128) and det.heatmaps.shape == (19, 96, 128)
+    assert poses.shape[0] == scores.shape[0] or poses.shape == (0,)
