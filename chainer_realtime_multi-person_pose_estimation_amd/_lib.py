@@ -25,6 +25,7 @@ EXPORTED = (
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
+    "op_set_conv_algo",
 )
 MAX_SCALES = 8
 PRECISION = {"fp32": 0, "bf16x3": 1}
@@ -77,6 +78,7 @@ def lib():
         "op_set_weights": ([P, P, P], ctypes.c_int),
         "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
         "op_detect_precise": ([P, P, I32, I32, I64, P, P, I32, P, P, P], ctypes.c_int),
+        "op_set_conv_algo": ([P, I32], ctypes.c_int),
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
         "op_forward": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
@@ -236,6 +238,10 @@ class Context(object):
         check(lib().op_detect(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], ptr(poses), ptr(scores),
                               cap, ctypes.byref(res)), "op_detect")
         return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+
+    def set_conv_algo(self, algo):
+        """Kernel family of the bf16x3 convolutions (include/openpose_hip.h: op_set_conv_algo)."""
+        check(lib().op_set_conv_algo(self.h, int(algo)), "op_set_conv_algo")
 
     def detect_precise(self, img, cap=2048, return_maps=False):
         """detect_precise (pose_detector.py:433-482): (poses, scores, res[, pafs (38,h,w), heatmaps (19,h,w)])."""

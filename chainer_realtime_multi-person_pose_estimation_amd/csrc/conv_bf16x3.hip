@@ -221,12 +221,17 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     }
     if (g[i].cop % 128) wide = false;
   }
-  if (s.halo_mode == 4 || (s.halo_mode == 5 && s.ks == 7)) {  // shared-weight halo tiles (conv_big.hip)
+  if (s.halo_mode == 6 && s.ks == 7) {  // 16x16x32 tap pairs (conv_pair.hip), then as mode 4
+    int taken = 0;
+    const int rc = launch_conv_pair(s, g, st, &taken);
+    if (rc || taken) return rc;
+  }
+  if (s.halo_mode == 4 || s.halo_mode == 6 || (s.halo_mode == 5 && s.ks == 7)) {  // conv_big.hip
     int taken = 0;
     const int rc = launch_conv_big(s, g, st, &taken);
     if (rc || taken) return rc;
   }
-  if (s.halo_mode == 3 || s.halo_mode == 4) {  // co-split halo kernel (conv_halo.hip), every kernel size
+  if (s.halo_mode == 3 || s.halo_mode == 4 || s.halo_mode == 6) {  // co-split halo kernel (conv_halo.hip)
     int taken = 0;
     const int rc = launch_conv_halo(s, g, st, &taken);
     if (rc || taken) return rc;

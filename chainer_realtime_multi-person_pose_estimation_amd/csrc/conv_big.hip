@@ -19,6 +19,7 @@
 //    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
 //  * MFMA: v_mfma_f32_32x32x16_bf16, products hi*hi + hi*lo + lo*hi into one f32 accumulator.
 #include <cstdlib>
+#include <vector>
 
 #include "common.hpp"
 
@@ -305,14 +306,21 @@ static int halo_bytes(int tr, int tc, int ks) {
   return 4 * 1024 * (((tr + ks - 1) * pitch + 63) / 64);
 }
 
-// Pick the tile (tr x tc) that fits LDS and wastes the fewest MFMA lanes; false if none fits.
+// Pick the tile (tr x tc) that fits LDS: among the tilings within 3 % of the best MFMA-lane
+// utilisation, the one with the least halo re-read ((tr+ks-1)(tc+ks-1) / (tr tc)); false if none fits.
 static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
   const int cap = k.cap();
   const int budget = k.lds_budget() - k.ring_bytes();
+  struct Cand {
+    int tr, tc, tiles_y, tiles_x;
+    double util, amp;
+  };
+  std::vector<Cand> cands;
   double best = 0.0;
-  for (int segs = 1; segs <= 16; ++segs) {
+  for (int segs = 1; segs <= 32; ++segs) {
     const int tc = (w + segs - 1) / segs;
     if (tc > cap || tc < 1) continue;
+    if (segs > 1 && (w + tc - 1) / tc != segs) continue;  // same tile width as a smaller segment count
     int tr = cap / tc;
     if (tr > h) tr = h;
     while (tr >= 1 && halo_bytes(tr, tc, k.ks) > budget) --tr;
@@ -320,15 +328,18 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
     const int tiles_y = (h + tr - 1) / tr;
     const int trb = (h + tiles_y - 1) / tiles_y;  // even the rows out over the same tile count
     const double util = (double)h * w / ((double)tiles_y * segs * cap);
-    if (util > best + 1e-9) {
-      best = util;
-      t.tr = trb;
-      t.tc = tc;
-      t.tiles_y = tiles_y;
-      t.tiles_x = (w + tc - 1) / tc;
-    }
+    const double amp = (double)(trb + k.ks - 1) * (tc + k.ks - 1) / ((double)trb * tc);
+    cands.push_back({trb, tc, tiles_y, segs, util, amp});
+    best = util > best ? util : best;
   }
   if (best <= 0.0) return false;
+  const Cand* pick = nullptr;
+  for (const Cand& c : cands)
+    if (c.util >= best - 0.03 && (!pick || c.amp < pick->amp - 1e-9)) pick = &c;
+  t.tr = pick->tr;
+  t.tc = pick->tc;
+  t.tiles_y = pick->tiles_y;
+  t.tiles_x = pick->tiles_x;
   t.pitch = t.tc + (k.ks > 1 ? 16 * ((k.ks - 1 + 15) / 16) : 0);
   t.hrows = t.tr + k.ks - 1;
   t.nh = (t.hrows * t.pitch + 63) / 64;
@@ -380,6 +391,14 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     return launch_big_t<7, 6, 8, 128, 1>(s, g, tl, st);
   }
   if (c128) {
+    static const int v3 = getenv("OP_BIG3") ? atoi(getenv("OP_BIG3")) : 0;  // tuning aid: 3x3 variant
+    if (v3 == 1 || v3 == 2) {
+      const BigConfig k{3, 6, 8, 128, v3 == 1 ? 1 : 0};
+      if (!big_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
+      if (plain_order) tl.xpu = 0;
+      *taken = 1;
+      return v3 == 1 ? launch_big_t<3, 6, 8, 128, 1>(s, g, tl, st) : launch_big_t<3, 6, 8, 128, 0>(s, g, tl, st);
+    }
     if (!big_tiling(BigConfig{3, 6, 4, 128, 0}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
     if (plain_order) tl.xpu = 0;
     *taken = 1;

@@ -270,6 +270,7 @@ struct op_ctx {
   int gn = 0, gh = 0, gw = 0;  // current geometry (batch, net h, net w)
   bool split = true;           // 3xBF16 split convs (default) or exact f32 MFMA convs
   bool gsplit = true;          // format the arena is currently carved for
+  int conv_algo = 4;           // split-path conv kernel family (op_set_conv_algo)
   Act buf[B_COUNT];
   // post-process
   PostBuffers pb{};
@@ -547,13 +548,10 @@ static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_
   return g;
 }
 
-// Split-path conv kernel family (OP_HALO_MODE env, tuning aid): 4 (default) shared-weight halo tiles
-// for 7x7 + 3x3 (conv_big.hip); 5 the same for 7x7 only; 3 co-split halo (conv_halo.hip); 1/2 the
-// 7x7 halo kernel with a single / double halo buffer; 0 the per-tap gather kernel everywhere.
-// Shapes a kernel does not take fall back to the gather kernel.
+// Default split-path conv kernel family of new contexts (op_set_conv_algo; OP_HALO_MODE env).
 static int g_halo_mode = 4;
 
-static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups) {
+static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups, int algo) {
   SplitConvShape s;
   s.n = n;
   s.h = out.h;
@@ -567,7 +565,7 @@ static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks
   s.relu = relu ? 1 : 0;
   s.groups = groups;
   s.cs_out32 = 0;
-  s.halo_mode = g_halo_mode;
+  s.halo_mode = algo;
   return s;
 }
 
@@ -580,7 +578,7 @@ static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout
     double fl = 0, by = 0;
     conv_work(c, out, pc, &fl, &by);
     return profiled(c, conv_class(pc.ks), fl, by, [&] {
-      return launch_conv_bf16x3(sshp(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, 1), g, c->stream);
+      return launch_conv_bf16x3(sshp(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, 1, c->conv_algo), g, c->stream);
     });
   }
   ConvGroup g[2];
@@ -599,7 +597,7 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
     SplitConvGroup g[2];
     g[0] = sgrp(in, ci0, out, co0, p0, st0);
     g[1] = sgrp(in, ci1, out, co1, p1, st1);
-    SplitConvShape sh = sshp(c->gn, in, out, p0.cin16 / 16, p0.ks, relu, 2);
+    SplitConvShape sh = sshp(c->gn, in, out, p0.cin16 / 16, p0.ks, relu, 2, c->conv_algo);
     if (out32) {
       g[0].out32 = g[1].out32 = out32->p;
       g[0].out32_off = o32a;
@@ -866,6 +864,7 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
   }
   for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
   if (const char* e = getenv("OP_HALO_MODE")) op::g_halo_mode = atoi(e);
+  c->conv_algo = op::g_halo_mode;
   if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
   if (const char* e = getenv("OP_GUARD")) op::g_guard = ((size_t)atol(e) + 255) / 256 * 256;
   // scipy _gaussian_kernel1d(sigma, 0, int(4*sigma + 0.5)) taps (restated; pinned by the tests)
@@ -1718,6 +1717,22 @@ int op_set_precision(op_ctx* c, int32_t mode) {
     return OP_ERR_INVALID;
   }
   c->split = mode == OP_PRECISION_BF16X3;
+  return OP_OK;
+}
+
+int op_set_conv_algo(op_ctx* c, int32_t algo) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (algo < 0 || algo > 6) {
+    set_error("conv algo must be 0..6");
+    return OP_ERR_INVALID;
+  }
+  c->conv_algo = algo;
+  if (c->gexec) {  // captured launches bake in the kernels
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
   return OP_OK;
 }
 

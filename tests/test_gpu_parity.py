@@ -103,6 +103,25 @@ def test_forward_368_vs_oracle(precision_ctx, rand_weights):
     _fwd_check(precision_ctx, rand_weights, x)
 
 
+@pytest.mark.parametrize("algo", [0, 1, 3, 5, 6])
+def test_conv_algos_agree(ctx, algo):
+    """Every bf16x3 kernel family computes the same forward (batch 2 at 368x368 and 720p-shaped
+    656x368) as the default family, within the 3xBF16 rounding (the default is held to the oracle
+    by test_forward_*_vs_oracle)."""
+    rng = np.random.default_rng(algo)
+    for shape in ((2, 3, 368, 368), (1, 3, 368, 656)):
+        x = rng.uniform(-0.5, 0.5, shape).astype(np.float32)
+        ctx.set_conv_algo(4)
+        p4, h4 = ctx.forward(x)
+        ctx.set_conv_algo(algo)
+        try:
+            pa, ha = ctx.forward(x)
+        finally:
+            ctx.set_conv_algo(4)
+        err = max(float(np.abs(p4 - pa).max()), float(np.abs(h4 - ha).max()))
+        assert err <= FWD_TOL, (algo, shape, err)
+
+
 def test_forward_precisions_agree(ctx, rand_weights):
     """bf16x3 vs exact-f32 MFMA on a 720p-shaped input (656x368), batch 2."""
     rng = np.random.default_rng(2)
