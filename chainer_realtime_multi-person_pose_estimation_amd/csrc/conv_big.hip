@@ -107,7 +107,7 @@ __device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const 
   }
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                                    SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -255,6 +255,56 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   }
   wait_vmcnt<0>();  // drain the trailing (never read) weight copies
 
+  if constexpr (POOL) {
+    // ---- fused 2x2 max-pool epilogue (the following F.max_pooling_2d, CocoPoseNet.py:138/141/146)
+    // Tiles are 32 wide, so block pb of a wave is one tile row: the window rows are blocks
+    // (pb, pb+1) of this lane and the window columns lanes (l32, l32^1).  Exactly the unfused
+    // path: ReLU(acc + b) split into hi/lo, the reconstructed hi+lo compared, the winner re-split.
+    const int wp_out = s.w / 2 + 2 * s.pout;
+    const int hp_out = s.h / 2 + 2 * s.pout;
+#pragma unroll
+    for (int pb = 0; pb < NPB; pb += 2) {
+      const int r = pg * NPB + pb;  // even tile row
+      const int x = x0 + l32;
+      const bool store = r < rows_here && x < s.w && (l32 & 1) == 0;
+      const int y = y0 + r;
+      char* optr = (char*)g.out +
+                   ((int64_t)(frame * hp_out + y / 2 + s.pout) * wp_out + (x / 2 + s.pout)) * (int64_t)s.cs_out * 4;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int co = co0 + ch * 64 + cb * 32 + 8 * q + 4 * hi;
+          const bool live = co < g.cout_store;
+          const floatx4 bv = live ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f};
+          u16x4g vh, vl;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float m = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              float f = acc[cb][pb + k][4 * q + e] + bv[e];
+              if (s.relu) f = f > 0.0f ? f : 0.0f;
+              const __bf16 h16 = (__bf16)f;
+              const float rc = (float)h16 + (float)(__bf16)(f - (float)h16);
+              m = k == 0 ? rc : fmaxf(m, rc);
+            }
+            m = fmaxf(m, __shfl_xor(m, 1));  // the window's other column (all lanes take part)
+            const __bf16 h16 = (__bf16)m;
+            const __bf16 l16 = (__bf16)(m - (float)h16);
+            vh[e] = __builtin_bit_cast(unsigned short, h16);
+            vl[e] = __builtin_bit_cast(unsigned short, l16);
+          }
+          if (store && live) {
+            char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+            *(u16x4g*)d = vh;
+            *(u16x4g*)(d + 16) = vl;
+          }
+        }
+    }
+    return;
+  }
+
   // ---- epilogue: bias, ReLU, split store (+ dense f32 copy) ----
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
@@ -350,23 +400,51 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   return true;
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false>
 static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
   const BigConfig k{KS, NPB, NWAVE, CW, PAIR};
   const int lds = k.ring_bytes() + 4 * tl.nh * 1024;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
+}
+
+// 3x3 conv + ReLU + 2x2 max-pool in one launch: s.h x s.w is the conv size, the output buffer is
+// (s.h/2) x (s.w/2) with halo s.pout.  Tiles are 32 columns x (pixel groups x NPB) rows.
+// *taken = 0 when the shape is outside this kernel (the caller runs conv + pool).
+int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
+  *taken = 0;
+  if (s.ks != 3 || s.groups != 1 || s.cs_in % 16 || s.pin < 1 || (s.h & 1) || (s.w & 1) || g[0].cop % 64 ||
+      g[0].cin_off % 16 || !s.relu)
+    return OP_OK;
+  const bool c128 = g[0].cop % 128 == 0;
+  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, 0} : BigConfig{3, 4, 4, 64, 0};
+  BigTiling t;
+  t.tc = 32;
+  t.tr = k.cap() / 32;  // rows = pixel groups x NPB (even)
+  if (halo_bytes(t.tr, t.tc, 3) > k.lds_budget() - k.ring_bytes()) return OP_OK;
+  t.tiles_y = (s.h + t.tr - 1) / t.tr;
+  t.tiles_x = (s.w + 31) / 32;
+  t.pitch = 48;
+  t.hrows = t.tr + 2;
+  t.nh = (t.hrows * t.pitch + 63) / 64;
+  t.co_tiles = g[0].cop / k.cw;
+  t.units = t.co_tiles;
+  t.per_unit = s.n * t.tiles_y * t.tiles_x;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  *taken = 1;
+  if (c128) return launch_big_t<3, 6, 4, 128, 0, true>(s, g, t, st);
+  return launch_big_t<3, 4, 4, 64, 0, true>(s, g, t, st);
 }
 
 // The split-path convolution on shared-weight halo tiles (7x7 and 3x3).  *taken = 0 when the

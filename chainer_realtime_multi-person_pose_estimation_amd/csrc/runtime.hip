@@ -590,6 +590,29 @@ static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout
                   [&] { return launch_conv(shp(c->gn, in, out, pc.cin_phys / 8, pc.ks, relu, 1), g, c->stream); });
 }
 
+static int pool(op_ctx* c, const Act& in, const Act& out, int ch);
+
+// conv (3x3, ReLU) followed by F.max_pooling_2d(2) (CocoPoseNet.py:137-138, 140-141, 145-146):
+// one fused launch on the split path with the conv_big families (the pooled tensor is the only
+// output), else the conv into `full` and the pool kernel.
+static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& pooled, const PackedConv& pc, int ch) {
+  if (c->split && (c->conv_algo == 4 || c->conv_algo == 6)) {
+    SplitConvGroup g[2];
+    g[0] = sgrp(in, 0, pooled, 0, pc, ch);
+    g[1] = g[0];
+    SplitConvShape sh = sshp(c->gn, in, full, pc.cin16 / 16, pc.ks, true, 1, c->conv_algo);
+    sh.pout = pooled.pad;
+    sh.cs_out = pooled.cs;
+    double fl = 0, by = 0;
+    conv_work(c, full, pc, &fl, &by);
+    int taken = 0;
+    const int rc = profiled(c, conv_class(pc.ks), fl, by, [&] { return launch_conv_big_pool(sh, g, c->stream, &taken); });
+    if (rc || taken) return rc;
+  }
+  const int rc = conv1(c, in, 0, full, 0, pc, ch, true);
+  return rc ? rc : pool(c, full, pooled, ch);
+}
+
 static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1, const PackedConv& p0,
                  const PackedConv& p1, int st0, int st1, bool relu, const Act* out32 = nullptr, int o32a = 0,
                  int o32b = 0) {
@@ -633,16 +656,13 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
 static int run_forward(op_ctx* c) {
   Act* B = c->buf;
   RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
-  RC(conv1(c, B[B_C11], 0, B[B_C12], 0, c->bb[1], 64, true));
-  RC(pool(c, B[B_C12], B[B_P1], 64));
+  RC(conv_pool(c, B[B_C11], B[B_C12], B[B_P1], c->bb[1], 64));
   RC(conv1(c, B[B_P1], 0, B[B_C21], 0, c->bb[2], 128, true));
-  RC(conv1(c, B[B_C21], 0, B[B_C22], 0, c->bb[3], 128, true));
-  RC(pool(c, B[B_C22], B[B_P2], 128));
+  RC(conv_pool(c, B[B_C21], B[B_C22], B[B_P2], c->bb[3], 128));
   RC(conv1(c, B[B_P2], 0, B[B_C3A], 0, c->bb[4], 256, true));
   RC(conv1(c, B[B_C3A], 0, B[B_C3B], 0, c->bb[5], 256, true));
   RC(conv1(c, B[B_C3B], 0, B[B_C3A], 0, c->bb[6], 256, true));
-  RC(conv1(c, B[B_C3A], 0, B[B_C34], 0, c->bb[7], 256, true));
-  RC(pool(c, B[B_C34], B[B_P3], 256));
+  RC(conv_pool(c, B[B_C3A], B[B_C34], B[B_P3], c->bb[7], 256));
   RC(conv1(c, B[B_P3], 0, B[B_C41], 0, c->bb[8], 512, true));
   RC(conv1(c, B[B_C41], 0, B[B_C42], 0, c->bb[9], 512, true));
   RC(conv1(c, B[B_C42], 0, B[B_C43], 0, c->bb[10], 256, true));

@@ -13,8 +13,8 @@ i1 = starts[-1] if len(starts) > 1 else len(rows)
 # logical conv FLOPs per frame, in launch order of the split plan (368x368)
 def f(ci, co, k, h):
     return 2.0 * ci * co * k * k * h * h
-plan = [f(3, 64, 3, 368), f(64, 64, 3, 368), None, f(64, 128, 3, 184), f(128, 128, 3, 184), None,
-        f(128, 256, 3, 92), f(256, 256, 3, 92), f(256, 256, 3, 92), f(256, 256, 3, 92), None,
+plan = [f(3, 64, 3, 368), f(64, 64, 3, 368), f(64, 128, 3, 184), f(128, 128, 3, 184),
+        f(128, 256, 3, 92), f(256, 256, 3, 92), f(256, 256, 3, 92), f(256, 256, 3, 92),
         f(256, 512, 3, 46), f(512, 512, 3, 46), f(512, 256, 3, 46), f(256, 128, 3, 46),
         f(128, 256, 3, 46), 2 * f(128, 128, 3, 46), 2 * f(128, 128, 3, 46), 2 * f(128, 512, 1, 46),
         f(512, 38, 1, 46) + f(512, 19, 1, 46)]
@@ -27,7 +27,7 @@ for r in rows[i0:i1]:
     dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
     tot += dt
     fl = ""
-    if "conv" in name or "maxpool" in name:
+    if "conv" in name:
         if j < len(plan):
             p = plan[j]
             j += 1
