@@ -108,6 +108,11 @@ int launch_preprocess(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
 int launch_preprocess_planar(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t dh,
                              int32_t dw, float* out_nchw, hipStream_t st);
 
+// conv1_1 as f32 FMAs (conv11.hip); frames != nullptr fuses the cv2 LINEAR network-input resize
+int launch_conv11_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t sh, int32_t sw,
+                        const float* x0, int32_t n, int32_t h, int32_t w, const float* wt, const float* bias,
+                        float* out, hipStream_t st);
+
 // ---- multi-scale path (precise.hip) ----
 int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
                             int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);

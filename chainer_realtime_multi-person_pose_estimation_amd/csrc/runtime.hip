@@ -264,6 +264,7 @@ struct op_ctx {
   PackedConv st_first[5];      // Mconv1 stage s, fused (Co 256, 192 phys in)
   PackedConv st_g[5][2][5];    // [stage][branch][Mconv2..Mconv6]
   PackedConv st_last[5][2];    // Mconv7
+  float* w11 = nullptr;        // conv1_1 weights [tap][ci][co] f32 for the VALU kernel (conv11.hip)
   // activation arena
   void* arena = nullptr;
   size_t arena_bytes = 0;
@@ -653,9 +654,22 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
   return launch_maxpool2(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
 }
 
-static int run_forward(op_ctx* c) {
+// frames != nullptr (split path): conv1_1 reads the uint8 frames directly (fused input kernel).
+static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame_bytes = 0, int64_t row_stride = 0,
+                       int sh = 0, int sw = 0) {
   Act* B = c->buf;
-  RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
+  static const bool c11_mfma = getenv("OP_CONV11_MFMA") != nullptr;  // debugging aid: the MFMA conv1_1
+  if (c->split && !(c11_mfma && !frames)) {
+    const Act& o = B[B_C11];
+    double fl = 0, by = 0;
+    conv_work(c, o, c->bb[0], &fl, &by);
+    RC(profiled(c, conv_class(3), fl, by, [&] {
+      return launch_conv11_split(frames, frame_bytes, row_stride, sh, sw, B[B_X0].p, c->gn, o.h, o.w, c->w11,
+                                 c->bb[0].b, o.p, c->stream);
+    }));
+  } else {
+    RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
+  }
   RC(conv_pool(c, B[B_C11], B[B_C12], B[B_P1], c->bb[1], 64));
   RC(conv1(c, B[B_P1], 0, B[B_C21], 0, c->bb[2], 128, true));
   RC(conv_pool(c, B[B_C21], B[B_C22], B[B_P2], c->bb[3], 128));
@@ -926,6 +940,8 @@ static void free_pc(op::PackedConv& p) {
 }
 
 static void free_weights(op_ctx* c) {
+  if (c->w11) hipFree(c->w11);
+  c->w11 = nullptr;
   for (auto& p : c->bb) free_pc(p);
   free_pc(c->s1_first);
   for (auto& a : c->s1_g)
@@ -1018,6 +1034,14 @@ int op_set_weights(op_ctx* c, const float* const* W, const float* const* b) {
     return upload(pc, w, bias);
   };
   for (int i = 0; i < 12; ++i) RC(single(c->bb[i], i, false));
+  {  // conv1_1 for the VALU kernel: [tap][ci][co]
+    std::vector<float> w11(9 * 3 * 64);
+    for (int co = 0; co < 64; ++co)
+      for (int ci = 0; ci < 3; ++ci)
+        for (int t = 0; t < 9; ++t) w11[(t * 3 + ci) * 64 + co] = W[0][(co * 3 + ci) * 9 + t];
+    OP_HIP_CHECK(hipMalloc(&c->w11, w11.size() * sizeof(float)));
+    OP_HIP_CHECK(hipMemcpy(c->w11, w11.data(), w11.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   const char* br[2] = {"L1", "L2"};
   RC(fused(c->s1_first, layer_index("conv5_1_CPM_L1"), layer_index("conv5_1_CPM_L2"), false));
   for (int bi = 0; bi < 2; ++bi) {
@@ -1352,13 +1376,13 @@ static int enqueue_staged(op_ctx* c, bool timing) {
   RC(ensure_geometry(c, c->st_n, in_h, in_w));
   RC(ensure_post(c, c->st_n, map_h, map_w));
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[0], c->stream));
-  if (c->split)
-    RC(launch_preprocess_split(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h,
-                               c->st_w, in_h, in_w, c->buf[B_X0].p, c->stream));
-  else
+  if (c->split) {  // the network input is resampled inside the conv1_1 kernel
+    RC(run_forward(c, c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_h, c->st_w));
+  } else {
     RC(launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h, c->st_w,
                          in_h, in_w, c->buf[B_X0].p, c->stream));
-  RC(run_forward(c));
+    RC(run_forward(c));
+  }
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[1], c->stream));
   const int lh = in_h / 8, lw = in_w / 8;
   MapSource src;
@@ -1826,3 +1850,14 @@ int op_last_timing(op_ctx* c, double* conv_ms, double* post_ms, double* total_ms
 }
 
 }  // extern "C"
+
+// Debugging aid (not part of the public header): copy the first `bytes` of activation buffer `id`
+// (BufId order) of the current geometry to the host.
+extern "C" int op_debug_read_buffer(op_ctx* c, int32_t id, void* dst, int64_t bytes) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (id < 0 || id >= B_COUNT || !dst || bytes < 0) return OP_ERR_INVALID;
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  OP_HIP_CHECK(hipMemcpy(dst, c->buf[id].p, (size_t)bytes, hipMemcpyDeviceToHost));
+  return OP_OK;
+}

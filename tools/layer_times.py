@@ -7,7 +7,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 B = int(sys.argv[2])
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # one step starts at the preprocess kernel; take the last complete step
-starts = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"] or "conv11" in r["Kernel_Name"]]
 i0 = starts[-2] if len(starts) > 1 else starts[0]
 i1 = starts[-1] if len(starts) > 1 else len(rows)
 # logical conv FLOPs per frame, in launch order of the split plan (368x368)
