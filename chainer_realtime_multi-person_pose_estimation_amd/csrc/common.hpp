@@ -90,6 +90,8 @@ int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // 3x3 conv + ReLU + 2x2 max-pool fused (conv_big.hip)
 int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
+// 3x3 / 7x7 with double-buffered 8-channel halos (conv_db.hip); pool: fused 2x2 max-pool
+int launch_conv_db(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, bool pool, int* taken);
 // 7x7 tap-pair kernel on v_mfma_f32_16x16x32_bf16 (conv_pair.hip)
 int launch_conv_pair(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,

@@ -221,6 +221,11 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     }
     if (g[i].cop % 128) wide = false;
   }
+  if (s.halo_mode == 7) {  // double-buffered 8-channel halos (conv_db.hip), 1x1 as mode 4
+    int taken = 0;
+    const int rc = launch_conv_db(s, g, st, false, &taken);
+    if (rc || taken) return rc;
+  }
   if (s.halo_mode == 6 && s.ks == 7) {  // 16x16x32 tap pairs (conv_pair.hip), then as mode 4
     int taken = 0;
     const int rc = launch_conv_pair(s, g, st, &taken);
@@ -231,7 +236,7 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     const int rc = launch_conv_big(s, g, st, &taken);
     if (rc || taken) return rc;
   }
-  if (s.halo_mode == 3 || s.halo_mode == 4 || s.halo_mode == 6) {  // co-split halo kernel (conv_halo.hip)
+  if (s.halo_mode == 3 || s.halo_mode == 4 || s.halo_mode >= 6) {  // co-split halo kernel (conv_halo.hip)
     int taken = 0;
     const int rc = launch_conv_halo(s, g, st, &taken);
     if (rc || taken) return rc;

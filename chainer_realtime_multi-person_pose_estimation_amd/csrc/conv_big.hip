@@ -207,6 +207,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     // ---- halo reload; everyone is past the previous chunk's reads ----
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef BIG_SKIP_RELOAD  // timing experiment only (wrong results): halo loaded for chunk 0 only
+    if (c == 0)
+#endif
     {
       const char* src0 = fbase + c * 64;
       for (int q = wave; q < 4 * tl.nh; q += NWAVE) {

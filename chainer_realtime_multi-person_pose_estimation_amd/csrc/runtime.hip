@@ -597,7 +597,7 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch);
 // one fused launch on the split path with the conv_big families (the pooled tensor is the only
 // output), else the conv into `full` and the pool kernel.
 static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& pooled, const PackedConv& pc, int ch) {
-  if (c->split && (c->conv_algo == 4 || c->conv_algo == 6)) {
+  if (c->split && (c->conv_algo == 4 || c->conv_algo >= 6)) {
     SplitConvGroup g[2];
     g[0] = sgrp(in, 0, pooled, 0, pc, ch);
     g[1] = g[0];
@@ -607,7 +607,10 @@ static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& poole
     double fl = 0, by = 0;
     conv_work(c, full, pc, &fl, &by);
     int taken = 0;
-    const int rc = profiled(c, conv_class(pc.ks), fl, by, [&] { return launch_conv_big_pool(sh, g, c->stream, &taken); });
+    const int rc = profiled(c, conv_class(pc.ks), fl, by, [&] {
+      return c->conv_algo == 7 ? launch_conv_db(sh, g, c->stream, true, &taken)
+                               : launch_conv_big_pool(sh, g, c->stream, &taken);
+    });
     if (rc || taken) return rc;
   }
   const int rc = conv1(c, in, 0, full, 0, pc, ch, true);
@@ -1767,8 +1770,8 @@ int op_set_precision(op_ctx* c, int32_t mode) {
 int op_set_conv_algo(op_ctx* c, int32_t algo) {
   using namespace op;
   RC(check_ctx(c, false));
-  if (algo < 0 || algo > 6) {
-    set_error("conv algo must be 0..6");
+  if (algo < 0 || algo > 7) {
+    set_error("conv algo must be 0..7");
     return OP_ERR_INVALID;
   }
   c->conv_algo = algo;
