@@ -1,0 +1,38 @@
+"""draw_person_pose (pose_detector.py:520-553): colours, skipped limbs, undetected joints."""
+import numpy as np
+
+from conftest import pkg_module
+
+
+def test_empty_poses_return_the_image():
+    D = pkg_module("draw")
+    img = np.zeros((10, 10, 3), np.uint8)
+    assert D.draw_person_pose(img, np.empty((0, 18, 3))) is img
+
+
+def test_joints_and_limbs_drawn_in_reference_colours():
+    D = pkg_module("draw")
+    img = np.zeros((80, 80, 3), np.uint8)
+    pose = np.zeros((1, 18, 3))
+    pose[0, 1] = (20, 20, 2)   # neck
+    pose[0, 8] = (20, 60, 2)   # right waist: limb 0 (1 -> 8), colour LIMB_COLORS[0]
+    pose[0, 2] = (60, 20, 2)   # right shoulder
+    pose[0, 16] = (60, 60, 2)  # right ear: limb 9 (2 -> 16) is never drawn
+    out = D.draw_person_pose(img, pose)
+    assert out is not img and img.sum() == 0
+    assert tuple(out[40, 20]) == tuple(D.LIMB_COLORS[0])       # middle of limb 0
+    assert tuple(out[40, 60]) == (0, 0, 0)                       # limb 9 skipped
+    assert tuple(out[20, 20]) == tuple(D.JOINT_COLORS[1])      # neck disc over the limb
+    assert tuple(out[60, 60]) == tuple(D.JOINT_COLORS[16])
+    assert tuple(out[20, 40]) == tuple(D.LIMB_COLORS[6])       # limb 6 (1 -> 2)
+    assert tuple(out[23, 20]) == tuple(D.JOINT_COLORS[1]) and tuple(out[24, 20]) == tuple(D.LIMB_COLORS[0])
+
+
+def test_undetected_joint_breaks_its_limbs():
+    D = pkg_module("draw")
+    img = np.zeros((50, 50, 3), np.uint8)
+    pose = np.zeros((1, 18, 3))
+    pose[0, 1] = (10, 10, 2)
+    pose[0, 8] = (10, 40, 0)  # not detected
+    out = D.draw_person_pose(img, pose)
+    assert tuple(out[25, 10]) == (0, 0, 0)

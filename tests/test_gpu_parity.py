@@ -245,3 +245,18 @@ def test_pose_detector_precise_mode(pkg, rand_weights):
         return  # random weights: the reference itself may raise / exceed caps on noise maps
     assert det.pafs.shape == (38, 96, 128) and det.heatmaps.shape == (19, 96, 128)
     assert poses.shape[0] == scores.shape[0] or poses.shape == (0,)
+
+
+def test_cli_writes_result_png(tmp_path, rand_weights):
+    """pose_detector.py:555-579: npz weights + image -> result image."""
+    from PIL import Image
+    W = pkg_module("weights")
+    D = pkg_module("draw")
+    wpath = str(tmp_path / "w.npz")
+    W.save_npz(wpath, rand_weights)
+    ipath = str(tmp_path / "in.png")
+    Image.fromarray(people_image()[:, :, ::-1]).save(ipath)
+    out = str(tmp_path / "result.png")
+    assert D.main(["posenet", wpath, "--img", ipath, "--out", out]) == 0
+    res = np.asarray(Image.open(out))
+    assert res.shape == people_image().shape
