@@ -25,7 +25,7 @@ EXPORTED = (
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
-    "op_set_conv_algo",
+    "op_set_conv_algo", "op_profile_classes",
 )
 MAX_SCALES = 8
 PRECISION = {"fp32": 0, "bf16x3": 1}
@@ -79,6 +79,7 @@ def lib():
         "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
         "op_detect_precise": ([P, P, I32, I32, I64, P, P, I32, P, P, P], ctypes.c_int),
         "op_set_conv_algo": ([P, I32], ctypes.c_int),
+        "op_profile_classes": ([P, I32], ctypes.c_int),
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
         "op_forward": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
@@ -393,6 +394,13 @@ class Context(object):
 
     def profile(self, enable=True):
         check(lib().op_profile_enable(self.h, 1 if enable else 0), "op_profile_enable")
+
+    def profile_classes(self, names):
+        """Time only these classes (names from PROFILE_CLASSES) while profiling is enabled."""
+        mask = 0
+        for n in names:
+            mask |= 1 << self.PROFILE_CLASSES.index(n)
+        check(lib().op_profile_classes(self.h, mask), "op_profile_classes")
 
     def profile_reset(self):
         check(lib().op_profile_reset(self.h), "op_profile_reset")

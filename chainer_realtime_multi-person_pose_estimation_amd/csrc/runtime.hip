@@ -295,6 +295,7 @@ struct op_ctx {
   bool timed = false;
   // per-class launch profiling
   bool prof = false;
+  int prof_mask = 0xF;  // kernel classes timed while prof (op_profile_classes)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<op::ProfPair> pending;
@@ -515,7 +516,7 @@ static hipEvent_t pool_event(op_ctx* c) {
 // Record an event pair around `fn`'s launches when profiling is on.
 template <class Fn>
 static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
-  if (!c->prof) return fn();
+  if (!c->prof || !((c->prof_mask >> cls) & 1)) return fn();
   hipEvent_t a = pool_event(c), b = pool_event(c);
   if (!a || !b) return fn();
   OP_HIP_CHECK(hipEventRecord(a, c->stream));
@@ -1794,6 +1795,13 @@ int op_profile_enable(op_ctx* c, int32_t enable) {
   using namespace op;
   RC(check_ctx(c, false));
   c->prof = enable != 0;
+  return OP_OK;
+}
+
+int op_profile_classes(op_ctx* c, int32_t mask) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  c->prof_mask = mask & 0xF;
   return OP_OK;
 }
 

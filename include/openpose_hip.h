@@ -197,6 +197,8 @@ int op_last_timing(op_ctx* ctx, double* conv_ms, double* post_ms, double* total_
 int op_profile_enable(op_ctx* ctx, int32_t enable);
 int op_profile_read(op_ctx* ctx, int32_t cls, double* ms, int64_t* launches, double* flops, double* bytes);
 int op_profile_reset(op_ctx* ctx);
+/* Which classes op_profile_enable times (bit c = class c; default 0xF = all). */
+int op_profile_classes(op_ctx* ctx, int32_t mask);
 
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
 double op_forward_flops(int32_t h, int32_t w);
