@@ -202,6 +202,10 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   for (int i = 0; i < AHEAD; ++i) stage_w(i);
   const char* const bp0 = halo + (2 * hi) * hplane;  // this lane's k-half: hi plane, lo plane follows
   const int wlane = (ch * 64 + l32) * 16;
+  constexpr int HSTEP = NWAVE / 4;
+  const int h_plane = wave & 3, h_i0 = wave >> 2;
+  const int h_sl0 = h_i0 * 64 + lane;
+  const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
   int it = 0;
   for (int c = 0; c < s.c16; ++c) {
     // ---- halo reload; everyone is past the previous chunk's reads ----
@@ -211,18 +215,27 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     if (c == 0)
 #endif
     {
-      const char* src0 = fbase + c * 64;
-      for (int q = wave; q < 4 * tl.nh; q += NWAVE) {
-        const int plane = q / tl.nh, i = q - (q / tl.nh) * tl.nh;
-        const int sl = i * 64 + lane;
-        const int hr = sl / tl.pitch, hc = sl - (sl / tl.pitch) * tl.pitch;
-        int yy = y0 - R + hr + s.pin, xx = x0 - R + hc + s.pin;
+#ifdef BIG_SAME_CHUNK  // timing experiment only (wrong results): every chunk re-reads chunk 0
+      const char* src0 = fbase + h_plane * 16;
+#else
+      const char* src0 = fbase + c * 64 + h_plane * 16;
+#endif
+      // wave w copies plane w%4, pieces w/4, w/4 + NWAVE/4, ...: the halo slot advances by a
+      // fixed stride, so (row, col) are stepped, not divided, per piece
+      int hr = h_r0, hc = h_c0;
+      char* dst = halo + h_plane * hplane + h_i0 * 1024;
+      for (int i = h_i0; i < tl.nh; i += HSTEP) {
         // slots past the padded image (bottom / right of a partial tile, pitch gap) only feed
         // masked outputs or are never read: clamp the source inside this frame
-        yy = yy < hp_in - 1 ? yy : hp_in - 1;
-        xx = xx < wp_in - 1 ? xx : wp_in - 1;
-        __builtin_amdgcn_global_load_lds((const void*)(src0 + plane * 16 + ((int64_t)yy * wp_in + xx) * pix_bytes),
-                                         LDS_PTR_G(halo + plane * hplane + i * 1024), 16, 0, 0);
+        const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
+                                         16, 0, 0);
+        dst += HSTEP * 1024;
+        hc += HSTEP * 64;
+        while (hc >= tl.pitch) {
+          hc -= tl.pitch;
+          ++hr;
+        }
       }
     }
     wait_vmcnt<0>();
