@@ -128,9 +128,7 @@ struct PostBuffers {
   int32_t maxp;        // peaks per joint cap
   int64_t maxc;        // candidates per limb cap (= maxp*maxp)
   int32_t maxs;        // subsets per frame cap (= 19*maxp)
-  float* up;           // [B][18][Hm][Wm] upsampled heat
-  float* tmp;          // [B][18][Hm][Wm] vertical pass
-  float* hm;           // [B][18][Hm][Wm] filtered
+  float* up;           // [B][18][Hm][Wm] full-res heat planes handed in through op_compute_peaks
   int32_t* peak_xy;    // [B][18][maxp]  x | y << 16
   float* peak_score;   // [B][18][maxp]
   int32_t* peak_cnt;   // [B][18]

@@ -37,29 +37,35 @@ struct UpTap {
   int u0, v0;
   float w1, w2, w3, w4;
 };
-
-// Chainer <= 6 ResizeImages weights for output (oy, ox).
-__device__ __forceinline__ UpTap up_tap(int oy, int ox, int H, int W, int oH, int oW) {
-  const double v = linspace_at(0.0, (double)(H - 1), oH, oy);
-  const double u = linspace_at(0.0, (double)(W - 1), oW, ox);
-  int v0 = (int)floor(v);
-  v0 = v0 > H - 2 ? H - 2 : v0;
-  v0 = v0 < 0 ? 0 : v0;
-  int u0 = (int)floor(u);
-  u0 = u0 > W - 2 ? W - 2 : u0;
-  u0 = u0 < 0 ? 0 : u0;
-  const double du1 = __dsub_rn((double)(u0 + 1), u), du0 = __dsub_rn(u, (double)u0);
-  const double dv1 = __dsub_rn((double)(v0 + 1), v), dv0 = __dsub_rn(v, (double)v0);
-  UpTap t;
-  t.u0 = u0;
-  t.v0 = v0;
-  t.w1 = __double2float_rn(__dmul_rn(du1, dv1));
-  t.w2 = __double2float_rn(__dmul_rn(du0, dv1));
-  t.w3 = __double2float_rn(__dmul_rn(du1, dv0));
-  t.w4 = __double2float_rn(__dmul_rn(du0, dv0));
+// One axis of the align-corners bilinear tap: source index i0 and the f64 distances to i0+1 / i0.
+struct AxisTap {
+  double d1, d0;
+  int i0, pad_;
+};
+__device__ __forceinline__ AxisTap axis_tap(int o, int L, int oL) {
+  const double u = linspace_at(0.0, (double)(L - 1), oL, o);
+  int i0 = (int)floor(u);
+  i0 = i0 > L - 2 ? L - 2 : i0;
+  i0 = i0 < 0 ? 0 : i0;
+  AxisTap t;
+  t.i0 = i0;
+  t.d1 = __dsub_rn((double)(i0 + 1), u);
+  t.d0 = __dsub_rn(u, (double)i0);
   return t;
 }
-
+__device__ __forceinline__ UpTap up_tap2(const AxisTap& ty, const AxisTap& tx) {
+  UpTap t;
+  t.u0 = tx.i0;
+  t.v0 = ty.i0;
+  t.w1 = __double2float_rn(__dmul_rn(tx.d1, ty.d1));
+  t.w2 = __double2float_rn(__dmul_rn(tx.d0, ty.d1));
+  t.w3 = __double2float_rn(__dmul_rn(tx.d1, ty.d0));
+  t.w4 = __double2float_rn(__dmul_rn(tx.d0, ty.d0));
+  return t;
+}
+__device__ __forceinline__ UpTap up_tap(int oy, int ox, int H, int W, int oH, int oW) {
+  return up_tap2(axis_tap(oy, H, oH), axis_tap(ox, W, oW));
+}
 __device__ __forceinline__ float up_combine(const UpTap& t, float x00, float x01, float x10, float x11) {
   float s = __fadd_rn(__fmul_rn(t.w1, x00), __fmul_rn(t.w2, x01));
   s = __fadd_rn(s, __fmul_rn(t.w3, x10));
@@ -448,12 +454,18 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   }
 }
 
-// ---- heat-map pipeline: (upsample + vertical Gaussian) -> (horizontal Gaussian + NMS) -> sort ----
-// Tiles are staged in LDS; the reflect boundary is resolved once per LDS row / column.
-constexpr int kVT = 64;   // vertical-pass tile (rows x cols)
-constexpr int kHTR = 16;  // horizontal-pass tile rows
-constexpr int kHTC = 64;  // horizontal-pass tile cols
-constexpr int kMaxR = 16; // max Gaussian radius of the tiled kernels
+// ---- heat-map pipeline: fused (upsample + vertical + horizontal Gaussian + NMS) -> sort ----
+// One block owns a kFT x kFT tile of one (frame, joint) plane.  The upsampled map is rebuilt in
+// LDS over the tile plus the 1-pixel NMS border plus the Gaussian radius on each side, the two
+// Gaussian passes run LDS to LDS in SciPy's order (f64 symmetric pairs, f32 between the passes),
+// and nothing but the peak list touches HBM.  The reflect boundary is resolved once per LDS row /
+// column: region row ly stands for image row reflect(y0 - 1 - r + ly), which is exactly the row the
+// reference's correlate1d reads for the tap (pose_detector.py:84, scipy mode='reflect').
+constexpr int kFT = 64;                    // output tile edge
+constexpr int kMaxR = 16;                  // max Gaussian radius of the tiled kernel
+constexpr int kFU = kFT + 2 + 2 * kMaxR;   // LDS region edge (upsampled map)
+constexpr int kFW = 48;                    // low-res window edge staged in LDS
+constexpr int kFN = 512;                   // threads per block (2 blocks / CU by LDS)
 
 __device__ __forceinline__ int reflect_near(int i, int L) {
   if (i < 0) i = -i - 1;
@@ -461,14 +473,13 @@ __device__ __forceinline__ int reflect_near(int i, int L) {
   return i < 0 ? 0 : (i >= L ? L - 1 : i);  // L > radius: one reflection suffices
 }
 
-struct HeatLow {
+struct HeatLow {  // heat channels of the low-res stage output, upsampled on the fly
+  static constexpr bool kLow = true;
   MapSource src;
   int lh, lw, mh, mw;
-  __device__ __forceinline__ float at(int f, int j, int y, int x) const {
-    return up_sample(low_map(src, lw, f), src.heat_off + j, up_tap(y, x, lh, lw, mh, mw));
-  }
 };
 struct HeatFull {  // already-upsampled planes [f*18 + j][mh][mw]
+  static constexpr bool kLow = false;
   const float* p;
   int mh, mw;
   __device__ __forceinline__ float at(int f, int j, int y, int x) const {
@@ -476,74 +487,161 @@ struct HeatFull {  // already-upsampled planes [f*18 + j][mh][mw]
   }
 };
 
-template <class Src>
-__global__ __launch_bounds__(256) void heat_vpass(Src src, int mh, int mw, const double* __restrict__ w, int r,
-                                                  float* __restrict__ tmp) {
-  __shared__ float tile[kVT + 2 * kMaxR][kVT];
+// R > 0: radius fixed at compile time (register-blocked passes, NV outputs per thread); R == 0: any
+// radius <= kMaxR given at run time (one output per thread).
+template <class Src, int R>
+__global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const double* __restrict__ w, int rr,
+                                                  float thresh, int cap, int32_t* __restrict__ stage_key,
+                                                  float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt) {
+  constexpr int kTP = kFU + 2;  // vertical-pass output pitch (16-byte aligned rows)
+  constexpr int kHP = kFT + 4;  // filtered-map pitch
+  constexpr int NB = 4;         // outputs per thread in the register-blocked passes
+  __shared__ float up[(kFU + NB) * kFU];         // upsampled region; reused for the filtered map
+  __shared__ float tmp[(kFT + 2 + 1) * kTP];     // vertical-pass output; low-res window before that
+  __shared__ AxisTap rt[kFU], ct[kFU];
+  __shared__ int wlo[2], whi[2];
+  const int r = R > 0 ? R : rr;
   const int fj = blockIdx.z;
   const int f = fj / OP_N_JOINTS, j = fj - f * OP_N_JOINTS;
-  const int x0 = blockIdx.x * kVT, y0 = blockIdx.y * kVT;
-  const int rows = kVT + 2 * r;
-  for (int i = threadIdx.x; i < rows * kVT; i += 256) {
-    const int ly = i / kVT, lx = i - ly * kVT;
-    const int x = x0 + lx;
-    float v = 0.0f;
-    if (x < mw) v = src.at(f, j, reflect_near(y0 - r + ly, mh), x);
-    tile[ly][lx] = v;
-  }
-  __syncthreads();
-  const int lx = threadIdx.x & (kVT - 1);
-  const int x = x0 + lx;
-  if (x >= mw) return;
-  for (int ly = threadIdx.x / kVT; ly < kVT; ly += 256 / kVT) {
-    const int y = y0 + ly;
-    if (y >= mh) break;
-    double o = __dmul_rn((double)tile[ly + r][lx], w[r]);
-    for (int jj = -r; jj < 0; ++jj)
-      o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)tile[ly + r + jj][lx], (double)tile[ly + r - jj][lx]), w[r + jj]));
-    tmp[((int64_t)fj * mh + y) * mw + x] = __double2float_rn(o);
-  }
-}
-
-// Horizontal pass + strict 4-neighbour NMS on a kHTR x kHTC tile; peaks are appended to the
-// (frame, joint) staging list as (y*mw + x, score) -- order restored by peak_sort.
-__global__ __launch_bounds__(256) void heat_hpass_nms(const float* __restrict__ tmp, int mh, int mw,
-                                                      const double* __restrict__ w, int r, float thresh, int cap,
-                                                      int32_t* __restrict__ stage_key, float* __restrict__ stage_score,
-                                                      int32_t* __restrict__ peak_cnt) {
-  __shared__ float src[kHTR + 2][kHTC + 2 + 2 * kMaxR];
-  __shared__ float hm[kHTR + 2][kHTC + 2];
-  const int fj = blockIdx.z;
-  const int x0 = blockIdx.x * kHTC, y0 = blockIdx.y * kHTR;
-  const int cols = kHTC + 2 + 2 * r;
-  const float* plane = tmp + (int64_t)fj * mh * mw;
-  for (int i = threadIdx.x; i < (kHTR + 2) * cols; i += 256) {
-    const int ly = i / cols, lx = i - ly * cols;
-    const int y = y0 - 1 + ly;
-    float v = 0.0f;
-    if (y >= 0 && y < mh) v = plane[(int64_t)y * mw + reflect_near(x0 - 1 - r + lx, mw)];
-    src[ly][lx] = v;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < (kHTR + 2) * (kHTC + 2); i += 256) {
-    const int ly = i / (kHTC + 2), lx = i - ly * (kHTC + 2);
-    const int y = y0 - 1 + ly, x = x0 - 1 + lx;
-    float v = 0.0f;  // outside the image a neighbour counts as 0 (pose_detector.py:87-94)
-    if (y >= 0 && y < mh && x >= 0 && x < mw) {
-      double o = __dmul_rn((double)src[ly][lx + r], w[r]);
-      for (int jj = -r; jj < 0; ++jj)
-        o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)src[ly][lx + r + jj], (double)src[ly][lx + r - jj]), w[r + jj]));
-      v = __double2float_rn(o);
+  const int x0 = blockIdx.x * kFT, y0 = blockIdx.y * kFT;
+  const int hr = min(kFT + 2, mh + 1 - y0);  // filtered rows needed: image rows y0-1 .. <= mh-1
+  const int hc = min(kFT + 2, mw + 1 - x0);
+  const int ur = hr + 2 * r, uc = hc + 2 * r;
+  const int uy0 = y0 - 1 - r, ux0 = x0 - 1 - r;
+  if constexpr (Src::kLow) {
+    if (threadIdx.x < 2) {
+      wlo[threadIdx.x] = 0x7fffffff;
+      whi[threadIdx.x] = -1;
     }
-    hm[ly][lx] = v;
+    __syncthreads();
+    for (int i = threadIdx.x; i < ur + uc; i += kFN) {
+      const bool row = i < ur;
+      const int k = row ? i : i - ur;
+      const AxisTap t = row ? axis_tap(reflect_near(uy0 + k, mh), src.lh, mh)
+                            : axis_tap(reflect_near(ux0 + k, mw), src.lw, mw);
+      (row ? rt : ct)[k] = t;
+      atomicMin(&wlo[row ? 0 : 1], t.i0);
+      atomicMax(&whi[row ? 0 : 1], t.i0 + 1);
+    }
+    __syncthreads();
+    const int wy = wlo[0], wx = wlo[1];
+    const int nwy = whi[0] - wy + 1, nwx = whi[1] - wx + 1;
+    const bool staged = nwy <= kFW && nwx <= kFW;  // block-uniform
+    const LowMap m = low_map(src.src, src.lw, f);
+    const int c = src.src.heat_off + j;
+    float* win = tmp;
+    if (staged)
+      for (int i = threadIdx.x; i < nwy * nwx; i += kFN) {
+        const int a = i / nwx;
+        win[i] = m.at(c, wy + a, wx + (i - a * nwx));
+      }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ur * uc; i += kFN) {
+      const int ly = i / uc, lx = i - ly * uc;
+      const UpTap t = up_tap2(rt[ly], ct[lx]);
+      float v;
+      if (staged) {
+        const float* q = win + (t.v0 - wy) * nwx + (t.u0 - wx);
+        v = up_combine(t, q[0], q[1], q[nwx], q[nwx + 1]);
+      } else {
+        v = up_sample(m, c, t);
+      }
+      up[ly * kFU + lx] = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < ur * uc; i += kFN) {
+      const int ly = i / uc, lx = i - ly * uc;
+      up[ly * kFU + lx] = src.at(f, j, reflect_near(uy0 + ly, mh), reflect_near(ux0 + lx, mw));
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kHTR * kHTC; i += 256) {
-    const int ly = i / kHTC + 1, lx = i % kHTC + 1;
+  if constexpr (R > 0) {
+    double wr[R + 1];
+#pragma unroll
+    for (int q = 0; q <= R; ++q) wr[q] = w[q];
+    // vertical pass: NB consecutive rows of one column per thread, the 2R+NB inputs read once
+    const int ngy = (hr + NB - 1) / NB;
+    for (int i = threadIdx.x; i < ngy * uc; i += kFN) {
+      const int g = i / uc, lx = i - g * uc;
+      const int ly0 = g * NB;
+      double v[2 * R + NB];
+#pragma unroll
+      for (int q = 0; q < 2 * R + NB; ++q) v[q] = (double)up[(ly0 + q) * kFU + lx];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        double o = __dmul_rn(v[q + R], wr[R]);
+#pragma unroll
+        for (int jj = -R; jj < 0; ++jj)
+          o = __dadd_rn(o, __dmul_rn(__dadd_rn(v[q + R + jj], v[q + R - jj]), wr[R + jj]));
+        if (ly0 + q < hr) tmp[(ly0 + q) * kTP + lx] = __double2float_rn(o);
+      }
+    }
+    __syncthreads();
+    // horizontal pass: NB consecutive columns of one row per thread (16-byte LDS reads)
+    constexpr int ngx = (kFT + 2 + NB - 1) / NB;
+    constexpr int NV4 = (2 * R + NB + 3) / 4;
+    for (int i = threadIdx.x; i < (kFT + 2) * ngx; i += kFN) {
+      const int ly = i / ngx, lx0 = (i - ly * ngx) * NB;
+      floatx4 out = {0.0f, 0.0f, 0.0f, 0.0f};  // outside the image a neighbour counts as 0 (pose_detector.py:87-94)
+      if (ly < hr && y0 - 1 + ly >= 0) {
+        float fv[NV4 * 4];
+        const floatx4* src4 = (const floatx4*)(tmp + ly * kTP + lx0);
+#pragma unroll
+        for (int q = 0; q < NV4; ++q) {
+          const floatx4 t = src4[q];
+          fv[4 * q + 0] = t[0];
+          fv[4 * q + 1] = t[1];
+          fv[4 * q + 2] = t[2];
+          fv[4 * q + 3] = t[3];
+        }
+        double v[2 * R + NB];
+#pragma unroll
+        for (int q = 0; q < 2 * R + NB; ++q) v[q] = (double)fv[q];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          double o = __dmul_rn(v[q + R], wr[R]);
+#pragma unroll
+          for (int jj = -R; jj < 0; ++jj)
+            o = __dadd_rn(o, __dmul_rn(__dadd_rn(v[q + R + jj], v[q + R - jj]), wr[R + jj]));
+          const int lx = lx0 + q;
+          if (lx < hc && x0 - 1 + lx >= 0) out[q] = __double2float_rn(o);
+        }
+      }
+      *(floatx4*)(up + ly * kHP + lx0) = out;
+    }
+  } else {
+    for (int i = threadIdx.x; i < hr * uc; i += kFN) {  // vertical pass
+      const int ly = i / uc, lx = i - ly * uc;
+      const float* col = up + (ly + r) * kFU + lx;
+      double o = __dmul_rn((double)col[0], w[r]);
+      for (int jj = -r; jj < 0; ++jj)
+        o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)col[jj * kFU], (double)col[-jj * kFU]), w[r + jj]));
+      tmp[ly * kTP + lx] = __double2float_rn(o);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (kFT + 2) * (kFT + 2); i += kFN) {  // horizontal pass
+      const int ly = i / (kFT + 2), lx = i - ly * (kFT + 2);
+      float v = 0.0f;  // outside the image a neighbour counts as 0 (pose_detector.py:87-94)
+      if (ly < hr && lx < hc && y0 - 1 + ly >= 0 && x0 - 1 + lx >= 0) {
+        const float* row = tmp + ly * kTP + lx + r;
+        double o = __dmul_rn((double)row[0], w[r]);
+        for (int jj = -r; jj < 0; ++jj)
+          o = __dadd_rn(o, __dmul_rn(__dadd_rn((double)row[jj], (double)row[-jj]), w[r + jj]));
+        v = __double2float_rn(o);
+      }
+      up[ly * kHP + lx] = v;
+    }
+  }
+  __syncthreads();
+  const float* hm = up;  // filtered map, (kFT + 2) rows of pitch kHP
+  constexpr int P = kHP;
+  for (int i = threadIdx.x; i < kFT * kFT; i += kFN) {  // strict 4-neighbour NMS (pose_detector.py:87-97)
+    const int ly = i / kFT + 1, lx = i % kFT + 1;
     const int y = y0 + ly - 1, x = x0 + lx - 1;
     if (y >= mh || x >= mw) continue;
-    const float v = hm[ly][lx];
-    if (v > thresh && v > hm[ly - 1][lx] && v > hm[ly + 1][lx] && v > hm[ly][lx - 1] && v > hm[ly][lx + 1]) {
+    const float v = hm[ly * P + lx];
+    if (v > thresh && v > hm[(ly - 1) * P + lx] && v > hm[(ly + 1) * P + lx] && v > hm[ly * P + lx - 1] &&
+        v > hm[ly * P + lx + 1]) {
       const int slot = atomicAdd(peak_cnt + fj, 1);
       if (slot < cap) {
         stage_key[(int64_t)fj * cap + slot] = y * mw + x;
@@ -600,13 +698,14 @@ template <class Src>
 static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
   const int planes = s.n * OP_N_JOINTS;
   OP_HIP_CHECK(hipMemsetAsync(b.peak_cnt, 0, sizeof(int32_t) * planes, st));
-  dim3 gv((unsigned)((s.mw + kVT - 1) / kVT), (unsigned)((s.mh + kVT - 1) / kVT), (unsigned)planes);
-  hipLaunchKernelGGL((heat_vpass<Src>), gv, dim3(256), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius, b.tmp);
-  OP_AFTER_LAUNCH("heat_vpass<Src>", st);
-  dim3 gh((unsigned)((s.mw + kHTC - 1) / kHTC), (unsigned)((s.mh + kHTR - 1) / kHTR), (unsigned)planes);
-  hipLaunchKernelGGL(heat_hpass_nms, gh, dim3(256), 0, st, b.tmp, s.mh, s.mw, b.gauss_w, s.radius, s.peak_thresh,
-                     b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
-  OP_AFTER_LAUNCH("heat_hpass_nms", st);
+  dim3 g((unsigned)((s.mw + kFT - 1) / kFT), (unsigned)((s.mh + kFT - 1) / kFT), (unsigned)planes);
+  if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
+    hipLaunchKernelGGL((heat_fused<Src, 10>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
+  else
+    hipLaunchKernelGGL((heat_fused<Src, 0>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
+  OP_AFTER_LAUNCH("heat_fused<Src>", st);
   hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,
                      b.peak_cnt, b.peak_xy, b.peak_score);
   OP_AFTER_LAUNCH("peak_sort", st);

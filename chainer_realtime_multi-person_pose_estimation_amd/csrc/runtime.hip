@@ -399,8 +399,6 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
   const size_t plane = (size_t)nn * OP_N_JOINTS * area * sizeof(float);
   std::vector<Part> parts = {
       {(void**)&b.up, plane},
-      {(void**)&b.tmp, plane},
-      {(void**)&b.hm, plane},
       {(void**)&b.peak_xy, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
       {(void**)&b.peak_score, (size_t)nn * OP_N_JOINTS * b.maxp * 4},
       {(void**)&b.peak_cnt, (size_t)nn * OP_N_JOINTS * 4},
@@ -420,7 +418,7 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
       {(void**)&b.res_hdr, (size_t)nn * 4 * 4},
       {(void**)&b.gauss_w, 64 * 8},
   };
-  static const char* const part_name[] = {"up",       "tmp",       "hm",        "peak_xy",    "peak_score",
+  static const char* const part_name[] = {"up",       "peak_xy",    "peak_score",
                                           "peak_cnt", "stage_key", "stage_score", "cand_score", "cand_idx",
                                           "cand_cnt", "conn_ab",   "conn_score", "conn_cnt",   "sub_ids",
                                           "sub_sc",   "res_poses", "res_scores", "res_subsets", "res_hdr",

@@ -67,6 +67,28 @@ def test_postprocess_from_network_maps_vs_reference(ctx, case):
     assert np.array_equal(scores, d["scores"])
 
 
+@pytest.mark.parametrize("sigma", [1.5, 4.0])
+def test_peaks_nondefault_sigma_vs_oracle(lib, sigma):
+    """gaussian_sigma != 2.5 runs the run-time-radius heat kernel (radius 6 and 16 = kMaxR); the
+    default radius 10 has its own register-blocked instantiation, covered by the goldens."""
+    params = dict(P.PARAMS, gaussian_sigma=sigma)
+    c = lib.Context(0, lib.params_from_dict(params), lib.OpLimits())
+    try:
+        for case in golden_cases()[:3]:
+            d = load_golden(case)
+            mh, mw = int(d["map_h"]), int(d["map_w"])
+            heat = P.resize_images(d["heat_low"], mh, mw)
+            want = P.compute_peaks_from_heatmaps(heat, params)
+            assert np.array_equal(c.compute_peaks(heat).reshape(-1, 5), want.reshape(-1, 5))
+            try:  # fused upsample + filter from the low-res maps: same peak count
+                _, _, res = c.postprocess(d["paf_low"], d["heat_low"], int(d["orig_h"]), int(d["orig_w"]))
+            except IndexError:  # the grouping quirk may fire on other peaks; the count is not reported then
+                continue
+            assert res.n_peaks == len(want)
+    finally:
+        c.close()
+
+
 def test_grouping_indexerror(ctx):
     d = load_golden("grouping_indexerror")
     off = d["conn_off"]
