@@ -59,7 +59,7 @@ def cpu_baseline(frames, maps, n_frames):
 
 
 KERNEL_7X7 = {0: "conv_bf16x3<7", 1: "conv7_halo_bf16x3", 2: "conv7_halo_bf16x3", 3: "conv_halo_bf16x3<7",
-              4: "conv_big_bf16x3<7", 5: "conv_big_bf16x3<7"}
+              4: "conv_big_bf16x3<7", 5: "conv_big_bf16x3<7", 8: "conv_big_bf16x3<7"}
 
 
 def committed_traffic(kernel, batch, precision, halo_mode):
@@ -76,7 +76,7 @@ def committed_traffic(kernel, batch, precision, halo_mode):
         cfg = d.get("config") or {}
         if cfg.get("frames_per_step_per_gpu") != batch or d.get("precision", "bf16x3") != precision:
             continue
-        if d.get("halo_mode", 1) != halo_mode:
+        if KERNEL_7X7.get(d.get("halo_mode", 1)) != KERNEL_7X7.get(halo_mode):  # same 7x7 kernel
             continue
         for k, v in d.get("kernels", {}).items():
             if k.replace("op::", "").startswith(kernel):

@@ -7,8 +7,12 @@
 // every A fragment NPB pixel blocks.
 //  * Activations: per 16-channel chunk the tile's input rows plus halo are copied once into LDS
 //    as 4 planes (hi/lo x k-half) of 16 B per pixel and all KSxKS taps read their shifted window
-//    from there.  The LDS row pitch is TC + 16 slots, so a 32-pixel block that wraps a tile row
-//    keeps every ds_read_b128 lane group on distinct banks.
+//    from there.  The LDS row pitch is TC + 16 slots when a 32-pixel block wraps a tile row (every
+//    ds_read_b128 lane group stays on distinct banks), the tight TC + KS - 1 when TC % 32 == 0.
+//  * DB (conv algo 8, 3x3 c128): two halo buffers; the next chunk's halo streams in, a few pieces
+//    per tap, while this chunk's taps run (2 x 4-wave workgroups per CU at 80 KiB each).  Parity-
+//    tested but ~2 % slower on the 3x3 layers than the default in an interleaved in-process A/B
+//    (tools/ab_algo.py): the reload latency is already covered by the co-resident workgroup.
 //  * Weights: (tap, chunk) tiles of CW channels x 4 planes stream through an LDS ring by
 //    global_load_lds (each wave copies its pieces), one counted vmcnt + one s_barrier per tap
 //    (PAIR = 0, 3-deep ring) or per pair of taps (PAIR = 1, 6-deep ring, 4 taps ahead).
@@ -33,7 +37,7 @@ typedef unsigned short u16x4g __attribute__((ext_vector_type(4)));
 struct BigTiling {
   int32_t tr, tc;            // tile rows x cols
   int32_t tiles_y, tiles_x;  // tiles per frame
-  int32_t pitch;             // LDS halo row pitch in 16-B slots: >= tc + ks - 1, (pitch - tc) % 16 == 0
+  int32_t pitch;             // LDS halo row pitch in 16-B slots (halo_pitch)
   int32_t hrows;             // tr + ks - 1
   int32_t nh;                // 1-KiB halo pieces per plane
   int32_t units;             // weight sets = groups x channel tiles
@@ -107,7 +111,7 @@ __device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const 
   }
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                                    SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -117,9 +121,11 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   constexpr int PLANE_W = CW * 16;       // bytes of one weight plane of the tile
   constexpr int SLOT_W = 4 * PLANE_W;    // one (tap, chunk) weight tile
   constexpr int NWP = 4 * CH / NWAVE;    // 1-KiB weight pieces per wave per tap
-  constexpr int RING = PAIR ? 6 : 3;
-  constexpr int AHEAD = PAIR ? 4 : 2;    // taps between a weight copy's issue and its use
+  // DB (double-buffered halo, 2 workgroups per CU at <= 80 KiB each) keeps a 2-slot weight ring
+  constexpr int RING = PAIR ? 6 : (DB ? 2 : 3);
+  constexpr int AHEAD = PAIR ? 4 : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
   static_assert(NWP >= 1 && NWP <= 2 && PG >= 1, "wave / channel split");
+  static_assert(!DB || !PAIR, "double-buffered halo runs one tap per barrier");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
 
   // ---- which tile / weight set ----
@@ -207,6 +213,63 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
   int it = 0;
+  if constexpr (DB) {
+    // ---- double-buffered halo: chunk c+1's halo streams into the other buffer during chunk c,
+    // a few 1-KiB pieces per tap right behind that tap's weight copy (taps 0 .. KSQ-2); the counted
+    // vmcnt of each tap leaves only the previous tap's pieces in flight, so all of them have landed
+    // (and passed a barrier) before chunk c+1's first tap.
+    const int hbytes = 4 * hplane;
+    const int np_w = (tl.nh - h_i0 + HSTEP - 1) / HSTEP;  // pieces of one chunk for this wave
+    const int ppt = (np_w + KSQ - 2) / (KSQ - 1);        // per tap, all issued by tap KSQ-2
+    auto halo_piece = [&](const char* src0, char* dst, int hr, int hc) {
+      const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
+                                       16, 0, 0);
+    };
+    {  // chunk 0, whole
+      int hr = h_r0, hc = h_c0;
+      char* dst = halo + h_plane * hplane + h_i0 * 1024;
+      for (int i = h_i0; i < tl.nh; i += HSTEP) {
+        halo_piece(fbase + h_plane * 16, dst, hr, hc);
+        dst += HSTEP * 1024;
+        hc += HSTEP * 64;
+        while (hc >= tl.pitch) {
+          hc -= tl.pitch;
+          ++hr;
+        }
+      }
+      wait_vmcnt<0>();
+    }
+    for (int c = 0; c < s.c16; ++c) {
+      const bool pf = c + 1 < s.c16;
+      const char* hsrc = fbase + (c + 1) * 64 + h_plane * 16;
+      char* hdst = halo + ((c + 1) & 1) * hbytes + h_plane * hplane + h_i0 * 1024;
+      int hr = h_r0, hc = h_c0, k = 0, n1 = 0;
+      const char* const bp = halo + (c & 1) * hbytes + (2 * hi) * hplane;
+#pragma unroll 1
+      for (int t = 0; t < KSQ; ++t, ++it) {
+        // W(it) (issued one tap back, before that tap's pieces) landed for this wave ...
+        wait_vm_dyn(n1);
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; slot (it+1) % 2 and the other halo are free
+        asm volatile("" ::: "memory");
+        stage_w(it + 1);
+        int n = 0;
+        if (pf)
+          for (; n < ppt && k < np_w; ++n, ++k) {
+            halo_piece(hsrc, hdst, hr, hc);
+            hdst += HSTEP * 1024;
+            hc += HSTEP * 64;
+            while (hc >= tl.pitch) {
+              hc -= tl.pitch;
+              ++hr;
+            }
+          }
+        n1 = n;
+        const char* wb = lds + (it % RING) * SLOT_W + wlane;
+        big_taps<NPB, KS, PLANE_W>(1, acc, bp, hplane, qp, wb, wb, t, tl.pitch, hi);
+      }
+    }
+  } else
   for (int c = 0; c < s.c16; ++c) {
     // ---- halo reload; everyone is past the previous chunk's reads ----
     __builtin_amdgcn_s_barrier();
@@ -248,7 +311,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
         // may be in flight; after a 1-tap tail the count over-waits, which is safe) ...
         wait_vmcnt<2 * NWP>();
         // ... and for every wave; every wave is also done with the slots of the previous pair
+#ifndef BIG_NO_TAP_BARRIER  // timing experiment only (races on the weight ring)
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         stage_w(it + 4);
         stage_w(it + 5);
@@ -261,7 +326,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll 1
       for (int t = 0; t < KSQ; ++t, ++it) {
         wait_vmcnt<NWP>();  // W(it) landed for this wave (W(it+1) may be in flight) ...
+#ifndef BIG_NO_TAP_BARRIER
         __builtin_amdgcn_s_barrier();  // ... and for every wave; slot (it-1) % 3 is free
+#endif
         asm volatile("" ::: "memory");
         stage_w(it + 2);
         const char* wb = lds + (it % RING) * SLOT_W + wlane;
@@ -361,22 +428,33 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 
 // ---- host side ----
 struct BigConfig {
-  int ks, npb, nwave, cw, pair;
+  int ks, npb, nwave, cw, pair, db = 0;
   int cap() const { return (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
-  int ring_bytes() const { return (pair ? 6 : 3) * 4 * cw * 16; }
+  int ring_bytes() const { return (pair ? 6 : (db ? 2 : 3)) * 4 * cw * 16; }
   int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
+  int halo_budget() const { return (lds_budget() - ring_bytes()) / (db ? 2 : 1); }
 };
 
+// LDS halo row pitch (16-B slots): a 32-pixel block that wraps a tile row (tc % 32 != 0) needs
+// (pitch - tc) % 16 == 0 to keep its ds_read_b128 lane groups on distinct banks; when tc % 32 == 0
+// every block is one contiguous row segment and the tight tc + ks - 1 suffices.
+static int halo_pitch(int tc, int ks) {
+  if (ks == 1) return tc;
+#ifdef BIG_GAP_PITCH  // timing experiment: the gapped pitch everywhere
+  return tc + 16 * ((ks - 1 + 15) / 16);
+#endif
+  return tc % 32 == 0 ? tc + ks - 1 : tc + 16 * ((ks - 1 + 15) / 16);
+}
+
 static int halo_bytes(int tr, int tc, int ks) {
-  const int pitch = tc + (ks > 1 ? 16 * ((ks - 1 + 15) / 16) : 0);
-  return 4 * 1024 * (((tr + ks - 1) * pitch + 63) / 64);
+  return 4 * 1024 * (((tr + ks - 1) * halo_pitch(tc, ks) + 63) / 64);
 }
 
 // Pick the tile (tr x tc) that fits LDS: among the tilings within 3 % of the best MFMA-lane
 // utilisation, the one with the least halo re-read ((tr+ks-1)(tc+ks-1) / (tr tc)); false if none fits.
 static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
   const int cap = k.cap();
-  const int budget = k.lds_budget() - k.ring_bytes();
+  const int budget = k.halo_budget();
   struct Cand {
     int tr, tc, tiles_y, tiles_x;
     double util, amp;
@@ -406,7 +484,7 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   t.tc = pick->tc;
   t.tiles_y = pick->tiles_y;
   t.tiles_x = pick->tiles_x;
-  t.pitch = t.tc + (k.ks > 1 ? 16 * ((k.ks - 1 + 15) / 16) : 0);
+  t.pitch = halo_pitch(t.tc, k.ks);
   t.hrows = t.tr + k.ks - 1;
   t.nh = (t.hrows * t.pitch + 63) / 64;
   t.co_tiles = (cop_max + k.cw - 1) / k.cw;
@@ -416,23 +494,44 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   return true;
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false>
 static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
-  const BigConfig k{KS, NPB, NWAVE, CW, PAIR};
-  const int lds = k.ring_bytes() + 4 * tl.nh * 1024;
+  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB};
+  const int lds = k.ring_bytes() + (DB ? 2 : 1) * 4 * tl.nh * 1024;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
+}
+
+// Conv algo 8: the 3x3 c128 layers on double-buffered halos.  Two 4-wave workgroups per CU at
+// 80 KiB each: 2-slot weight ring (16 KiB) + 2 x 32 KiB halos of a 12 x 32 tile.  32-pixel blocks
+// are whole tile rows, so the halo pitch needs no bank-conflict gap: tc + 2 = 34 slots.
+static bool db_tiling(const SplitConvShape& s, int groups, int cop_max, BigTiling& t) {
+  if (s.halo_mode != 8 || s.ks != 3 || cop_max % 128) return false;
+  t.tc = 32;
+  t.tr = 12;
+  t.tiles_x = (s.w + 31) / 32;
+  t.tiles_y = (s.h + t.tr - 1) / t.tr;
+  if ((double)s.w / (t.tiles_x * 32) < 0.9) return false;  // narrow maps (46 wide): single buffer
+  t.pitch = halo_pitch(32, 3);
+  t.hrows = t.tr + 2;
+  t.nh = (t.hrows * t.pitch + 63) / 64;
+  if (2 * 128 * 16 * 4 + 2 * 4 * t.nh * 1024 > 80 * 1024) return false;
+  t.co_tiles = (cop_max + 127) / 128;
+  t.units = groups * t.co_tiles;
+  t.per_unit = s.n * t.tiles_y * t.tiles_x;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  return true;
 }
 
 // 3x3 conv + ReLU + 2x2 max-pool in one launch: s.h x s.w is the conv size, the output buffer is
@@ -444,14 +543,18 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
       g[0].cin_off % 16 || !s.relu)
     return OP_OK;
   const bool c128 = g[0].cop % 128 == 0;
-  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, 0} : BigConfig{3, 4, 4, 64, 0};
   BigTiling t;
+  if (c128 && db_tiling(s, 1, g[0].cop, t)) {
+    *taken = 1;
+    return launch_big_t<3, 6, 4, 128, 0, true, true>(s, g, t, st);
+  }
+  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, 0} : BigConfig{3, 4, 4, 64, 0};
   t.tc = 32;
   t.tr = k.cap() / 32;  // rows = pixel groups x NPB (even)
-  if (halo_bytes(t.tr, t.tc, 3) > k.lds_budget() - k.ring_bytes()) return OP_OK;
+  if (halo_bytes(t.tr, t.tc, 3) > k.halo_budget()) return OP_OK;
   t.tiles_y = (s.h + t.tr - 1) / t.tr;
   t.tiles_x = (s.w + 31) / 32;
-  t.pitch = 48;
+  t.pitch = halo_pitch(32, 3);
   t.hrows = t.tr + 2;
   t.nh = (t.hrows * t.pitch + 63) / 64;
   t.co_tiles = g[0].cop / k.cw;
@@ -492,6 +595,11 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       return v3 == 1 ? launch_big_t<3, 6, 8, 128, 1>(s, g, tl, st) : launch_big_t<3, 6, 8, 128, 0>(s, g, tl, st);
+    }
+    if (db_tiling(s, s.groups, cop_max, tl)) {
+      if (plain_order) tl.xpu = 0;
+      *taken = 1;
+      return launch_big_t<3, 6, 4, 128, 0, false, true>(s, g, tl, st);
     }
     if (!big_tiling(BigConfig{3, 6, 4, 128, 0}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
     if (plain_order) tl.xpu = 0;

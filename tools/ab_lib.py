@@ -1,0 +1,28 @@
+"""Interleaved A/B of library builds (OP_LIB_VARIANT) with per-class times: each variant runs in
+its own child process per round (a process loads one library).  usage: ab_lib.py ROUNDS base v1 ..."""
+import json
+import os
+import subprocess
+import sys
+
+rounds = int(sys.argv[1])
+variants = sys.argv[2:]
+here = os.path.dirname(os.path.abspath(__file__))
+out = {v: [] for v in variants}
+for r in range(rounds):
+    for v in variants:
+        env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
+        p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--steps", "10",
+                            "--warmup", "2"], env=env, capture_output=True, text=True, timeout=300)
+        if p.returncode:
+            print(p.stdout[-2000:], p.stderr[-2000:])
+            sys.exit(p.returncode)
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+        out[v].append((d["value"], d["stage_ms_per_step"]))
+        print(r, v, d["value"], d["stage_ms_per_step"], flush=True)
+for v in variants:
+    vals = sorted(x[0] for x in out[v])
+    c3 = sorted(x[1]["conv3x3"] for x in out[v])
+    c7 = sorted(x[1]["conv7x7"] for x in out[v])
+    print("%-8s fps median %.1f | conv3x3 median %.3f | conv7x7 median %.3f" % (v, vals[len(vals) // 2], c3[len(c3) // 2],
+                                                                           c7[len(c7) // 2]))
