@@ -450,8 +450,13 @@ static int halo_bytes(int tr, int tc, int ks) {
   return 4 * 1024 * (((tr + ks - 1) * halo_pitch(tc, ks) + 63) / 64);
 }
 
+#ifndef BIG_UTIL_WIN
+#define BIG_UTIL_WIN 0.03
+#endif
+
 // Pick the tile (tr x tc) that fits LDS: among the tilings within 3 % of the best MFMA-lane
-// utilisation, the one with the least halo re-read ((tr+ks-1)(tc+ks-1) / (tr tc)); false if none fits.
+// utilisation, the one that loads the fewest halo slots per tile pixel (hrows x pitch / (tr tc)).
+// Widths are the even splits of the image (ceil(w / segs)) and the multiples of 32 (tight pitch).
 static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
   const int cap = k.cap();
   const int budget = k.halo_budget();
@@ -461,10 +466,12 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   };
   std::vector<Cand> cands;
   double best = 0.0;
-  for (int segs = 1; segs <= 32; ++segs) {
-    const int tc = (w + segs - 1) / segs;
+  std::vector<int> widths;
+  for (int segs = 1; segs <= 32; ++segs) widths.push_back((w + segs - 1) / segs);
+  for (int tc = 32; tc < w && tc <= cap; tc += 32) widths.push_back(tc);
+  for (int tc : widths) {
     if (tc > cap || tc < 1) continue;
-    if (segs > 1 && (w + tc - 1) / tc != segs) continue;  // same tile width as a smaller segment count
+    const int segs = (w + tc - 1) / tc;
     int tr = cap / tc;
     if (tr > h) tr = h;
     while (tr >= 1 && halo_bytes(tr, tc, k.ks) > budget) --tr;
@@ -472,14 +479,14 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
     const int tiles_y = (h + tr - 1) / tr;
     const int trb = (h + tiles_y - 1) / tiles_y;  // even the rows out over the same tile count
     const double util = (double)h * w / ((double)tiles_y * segs * cap);
-    const double amp = (double)(trb + k.ks - 1) * (tc + k.ks - 1) / ((double)trb * tc);
+    const double amp = (double)(trb + k.ks - 1) * halo_pitch(tc, k.ks) / ((double)trb * tc);
     cands.push_back({trb, tc, tiles_y, segs, util, amp});
     best = util > best ? util : best;
   }
   if (best <= 0.0) return false;
   const Cand* pick = nullptr;
   for (const Cand& c : cands)
-    if (c.util >= best - 0.03 && (!pick || c.amp < pick->amp - 1e-9)) pick = &c;
+    if (c.util >= best - BIG_UTIL_WIN && (!pick || c.amp < pick->amp - 1e-9)) pick = &c;
   t.tr = pick->tr;
   t.tc = pick->tc;
   t.tiles_y = pick->tiles_y;
