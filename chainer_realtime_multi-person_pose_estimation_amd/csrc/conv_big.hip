@@ -15,9 +15,11 @@
 //    (tools/ab_algo.py): the reload latency is already covered by the co-resident workgroup.
 //  * Weights: (tap, chunk) tiles of CW channels x 4 planes stream through an LDS ring by
 //    global_load_lds (each wave copies its pieces), one counted vmcnt + one s_barrier per tap
-//    (PAIR = 0, 3-deep ring) or per pair of taps (PAIR = 1, 6-deep ring, 4 taps ahead).
+//    (PAIR = 0, 3-deep ring) or per pair of taps (PAIR = 1, 6-deep ring, 4 taps ahead; raster
+//    tiles, whose two-frame halo needs the LDS, 4-deep ring, 2 taps ahead).
 //  * The weight bytes fetched per MFMA-flop fall with the tile's pixel count: 7x7 uses one
-//    8-wave workgroup per CU on 768-pixel tiles; 3x3 uses two 4-wave workgroups per CU on
+//    8-wave workgroup per CU on 768-pixel raster tiles (consecutive pixels of the batch, crossing
+//    frame borders, so no lane computes padding); 3x3 uses two 4-wave workgroups per CU on
 //    384-pixel tiles so one workgroup's halo reload (every 9 taps) overlaps the other's MFMAs.
 //  * Workgroup -> XCD: blocks are dealt to XCDs round-robin, so block b is remapped to make every
 //    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
@@ -44,6 +46,7 @@ struct BigTiling {
   int32_t co_tiles;          // channel tiles per group
   int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
   int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
+  int32_t hw, total;         // raster tiles: pixels per frame, pixels of the batch
 };
 
 template <int N>
@@ -111,7 +114,7 @@ __device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const 
   }
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB, bool RASTER>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                                    SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -122,10 +125,13 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   constexpr int SLOT_W = 4 * PLANE_W;    // one (tap, chunk) weight tile
   constexpr int NWP = 4 * CH / NWAVE;    // 1-KiB weight pieces per wave per tap
   // DB (double-buffered halo, 2 workgroups per CU at <= 80 KiB each) keeps a 2-slot weight ring
-  constexpr int RING = PAIR ? 6 : (DB ? 2 : 3);
-  constexpr int AHEAD = PAIR ? 4 : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
+  // RASTER (tiles over the batch's raster order, 2 halo regions) keeps a 4-slot ring for pairs
+  constexpr int RING = PAIR ? (RASTER ? 4 : 6) : (DB ? 2 : 3);
+  constexpr int AHEAD = PAIR ? (RASTER ? 2 : 4) : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
+  constexpr int CAP = PG * NPB * 32;     // output pixels per tile
   static_assert(NWP >= 1 && NWP <= 2 && PG >= 1, "wave / channel split");
   static_assert(!DB || !PAIR, "double-buffered halo runs one tap per barrier");
+  static_assert(!RASTER || (!DB && !POOL), "raster tiles: single halo buffer, plain epilogue");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
 
   // ---- which tile / weight set ----
@@ -144,11 +150,25 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   const int co0 = (unit - grp * tl.co_tiles) * CW;
   const SplitConvGroup g = grp == 0 ? g0 : g1;
   if (co0 >= g.cop) return;  // narrower second group
-  const int tpf = tl.tiles_y * tl.tiles_x;
-  const int frame = widx / tpf;
-  const int tix = widx - frame * tpf;
-  const int ty = tix / tl.tiles_x;
-  const int y0 = ty * tl.tr, x0 = (tix - ty * tl.tiles_x) * tl.tc;
+  // rect tiles: frame, rows y0.., cols x0..; raster tiles: batch raster pixels P0..P1, i.e. rows
+  // y0.. of `frame` and, when the range runs into the next frame, rows 0.. of frame fb, whose halo
+  // rows follow frame's (from halo row rowsA on)
+  int frame, y0, x0 = 0, fb = 0, rowsA = 1 << 30, P0 = 0, P1 = 0;
+  if constexpr (RASTER) {
+    P0 = widx * CAP;
+    P1 = min(P0 + CAP, tl.total) - 1;
+    frame = P0 / tl.hw;
+    y0 = (P0 - frame * tl.hw) / s.w;
+    fb = P1 / tl.hw;
+    if (fb != frame) rowsA = s.h - y0 + 2 * R;
+  } else {
+    const int tpf = tl.tiles_y * tl.tiles_x;
+    frame = widx / tpf;
+    const int tix = widx - frame * tpf;
+    const int ty = tix / tl.tiles_x;
+    y0 = ty * tl.tr;
+    x0 = (tix - ty * tl.tiles_x) * tl.tc;
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -161,6 +181,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   const int hp_in = s.h + 2 * s.pin;
   const int64_t pix_bytes = (int64_t)s.cs_in * 4;
   const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
+  const char* const fbase_b = (const char*)g.in + (int64_t)fb * hp_in * wp_in * pix_bytes;
 
   // weights: wave w copies pieces j = w*NWP + i: plane j / CH, channels co0 + 64*(j % CH) + 0..63
   const int64_t wplane = (int64_t)g.cop * 16;
@@ -190,8 +211,18 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     const int p = (pg * NPB + pb) * 32 + l32;
-    const int r = p / tl.tc, c = p - (p / tl.tc) * tl.tc;
-    const uint32_t q = (r < rows_here && c < cols_here) ? (uint32_t)(r * tl.pitch + c) : 0u;  // pad lanes: never stored
+    uint32_t q = 0u;  // pad lanes: never stored
+    if constexpr (RASTER) {
+      const int P = P0 + p;
+      if (P <= P1) {
+        const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
+        const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
+        q = (uint32_t)((f == frame ? y - y0 : rowsA + y) * tl.pitch + x);
+      }
+    } else {
+      const int r = p / tl.tc, c = p - (p / tl.tc) * tl.tc;
+      if (r < rows_here && c < cols_here) q = (uint32_t)(r * tl.pitch + c);
+    }
     if (pb & 1) qp[pb >> 1] |= q << 16;
     else qp[pb >> 1] = q;
   }
@@ -283,6 +314,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #else
       const char* src0 = fbase + c * 64 + h_plane * 16;
 #endif
+      const char* src0_b = fbase_b + c * 64 + h_plane * 16;
       // wave w copies plane w%4, pieces w/4, w/4 + NWAVE/4, ...: the halo slot advances by a
       // fixed stride, so (row, col) are stepped, not divided, per piece
       int hr = h_r0, hc = h_c0;
@@ -290,9 +322,11 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
       for (int i = h_i0; i < tl.nh; i += HSTEP) {
         // slots past the padded image (bottom / right of a partial tile, pitch gap) only feed
         // masked outputs or are never read: clamp the source inside this frame
-        const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
-                                         16, 0, 0);
+        const bool in_a = hr < rowsA;  // raster tiles: halo rows past rowsA belong to frame fb
+        const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
+        const int xx = min(x0 - R + hc + s.pin, wp_in - 1);
+        __builtin_amdgcn_global_load_lds((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes),
+                                         LDS_PTR_G(dst), 16, 0, 0);
         dst += HSTEP * 1024;
         hc += HSTEP * 64;
         while (hc >= tl.pitch) {
@@ -309,14 +343,14 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
       for (int t = 0; t < KSQ; t += 2) {
         // taps (t, t+1) share one barrier: W(it), W(it+1) landed for this wave (W(it+2), W(it+3)
         // may be in flight; after a 1-tap tail the count over-waits, which is safe) ...
-        wait_vmcnt<2 * NWP>();
+        wait_vmcnt<AHEAD == 4 ? 2 * NWP : 0>();
         // ... and for every wave; every wave is also done with the slots of the previous pair
 #ifndef BIG_NO_TAP_BARRIER  // timing experiment only (races on the weight ring)
         __builtin_amdgcn_s_barrier();
 #endif
         asm volatile("" ::: "memory");
-        stage_w(it + 4);
-        stage_w(it + 5);
+        stage_w(it + AHEAD);
+        stage_w(it + AHEAD + 1);
         const int nt = t + 1 < KSQ ? 2 : 1;
         big_taps<NPB, KS, PLANE_W>(nt, acc, bp0, hplane, qp, lds + (it % RING) * SLOT_W + wlane,
                                    lds + ((it + 1) % RING) * SLOT_W + wlane, t, tl.pitch, hi);
@@ -394,11 +428,22 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll
   for (int pb = 0; pb < NPB; ++pb) {
     const int p = (pg * NPB + pb) * 32 + l32;
-    const int r = p / tl.tc, cc = p - (p / tl.tc) * tl.tc;
-    if (r >= rows_here || cc >= cols_here) continue;
-    const int y = y0 + r, x = x0 + cc;
-    char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
-    float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
+    int f = frame, y, x;
+    if constexpr (RASTER) {
+      const int P = P0 + p;
+      if (P > P1) continue;
+      f = P / tl.hw;
+      const int pp = P - f * tl.hw;
+      y = pp / s.w;
+      x = pp - y * s.w;
+    } else {
+      const int r = p / tl.tc, cc = p - (p / tl.tc) * tl.tc;
+      if (r >= rows_here || cc >= cols_here) continue;
+      y = y0 + r;
+      x = x0 + cc;
+    }
+    char* optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
+    float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -428,9 +473,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 
 // ---- host side ----
 struct BigConfig {
-  int ks, npb, nwave, cw, pair, db = 0;
+  int ks, npb, nwave, cw, pair, db = 0, raster = 0;
   int cap() const { return (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
-  int ring_bytes() const { return (pair ? 6 : (db ? 2 : 3)) * 4 * cw * 16; }
+  int ring_bytes() const { return (pair ? (raster ? 4 : 6) : (db ? 2 : 3)) * 4 * cw * 16; }
   int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
   int halo_budget() const { return (lds_budget() - ring_bytes()) / (db ? 2 : 1); }
 };
@@ -501,23 +546,59 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   return true;
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false, bool RASTER = false>
 static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
-  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB};
+  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB, RASTER};
   const int lds = k.ring_bytes() + (DB ? 2 : 1) * 4 * tl.nh * 1024;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
+}
+
+// Raster tiles: tile i = pixels [i*cap, (i+1)*cap) of the batch in raster order, so a tile can run
+// from the bottom rows of one frame into the top rows of the next and no MFMA lane computes padding
+// (46 x 46 maps: 2116 px = 2.76 tiles of 768, where rectangular tiles pay 3).  The halo holds the
+// tile's rows of each frame with their own KS-1 border rows; every frame is >= cap pixels, so a
+// tile touches at most two.  false when the worst tile's halo does not fit LDS.
+static bool raster_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
+  const int cap = k.cap(), hw = h * w, R = k.ks / 2;
+  const int64_t total = (int64_t)n * hw;
+  if (hw < cap || total >= (1 << 30)) return false;
+  const int tiles = (int)((total + cap - 1) / cap);
+  int rows_max = 0;
+  for (int i = 0; i < tiles; ++i) {
+    const int P0 = i * cap, P1 = (int)std::min<int64_t>((int64_t)P0 + cap, total) - 1;
+    const int fa = P0 / hw, ya = (P0 - fa * hw) / w, fb = P1 / hw, yb = (P1 - fb * hw) / w;
+    const int rows = fa == fb ? yb - ya + 1 + 2 * R : (h - ya + 2 * R) + (yb + 1 + 2 * R);
+    rows_max = std::max(rows_max, rows);
+  }
+  const int pitch = halo_pitch(w, k.ks);
+  const int nh = (rows_max * pitch + 63) / 64;
+  if (4 * nh * 1024 > k.lds_budget() - k.ring_bytes() || nh * 64 >= 65536) return false;
+  t.tr = 0;
+  t.tc = w;
+  t.tiles_y = tiles;
+  t.tiles_x = 1;
+  t.pitch = pitch;
+  t.hrows = rows_max;
+  t.nh = nh;
+  t.co_tiles = (cop_max + k.cw - 1) / k.cw;
+  t.units = groups * t.co_tiles;
+  t.per_unit = tiles;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  t.hw = hw;
+  t.total = (int)total;
+  return true;
 }
 
 // Conv algo 8: the 3x3 c128 layers on double-buffered halos.  Two 4-wave workgroups per CU at
@@ -550,7 +631,7 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
       g[0].cin_off % 16 || !s.relu)
     return OP_OK;
   const bool c128 = g[0].cop % 128 == 0;
-  BigTiling t;
+  BigTiling t{};
   if (c128 && db_tiling(s, 1, g[0].cop, t)) {
     *taken = 1;
     return launch_big_t<3, 6, 4, 128, 0, true, true>(s, g, t, st);
@@ -586,9 +667,14 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     cop_max = cop_max > g[i].cop ? cop_max : g[i].cop;
   }
   static const bool plain_order = getenv("OP_BIG_PLAIN_ORDER") != nullptr;  // tuning aid: no XCD remap
-  BigTiling tl;
+  BigTiling tl{};
   if (s.ks == 7) {
     if (!c128) return OP_OK;
+    if (s.halo_mode != 9 && raster_tiling(BigConfig{7, 6, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
+      if (plain_order) tl.xpu = 0;
+      *taken = 1;
+      return launch_big_t<7, 6, 8, 128, 1, false, false, true>(s, g, tl, st);
+    }
     if (!big_tiling(BigConfig{7, 6, 8, 128, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
     if (plain_order) tl.xpu = 0;
     *taken = 1;
