@@ -114,7 +114,46 @@ __device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const 
   }
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB, bool RASTER>
+// One tap for one wave with the A fragments already in registers (WREG): 2 channel blocks x NPB
+// pixel blocks; bh/bl[0] hold block 0 of this tap on entry and, when `next`, block 0 of tap t+1
+// on exit (same halo), so no tap starts on an LDS round trip.
+template <int NPB, int KS>
+__device__ __forceinline__ void wv_tap(floatx16 (&acc)[2][NPB], const char* bp0, int hplane,
+                                       const uint32_t (&qp)[(NPB + 1) / 2], const bf16x8g (&ah)[2],
+                                       const bf16x8g (&al)[2], bf16x8g (&bh)[2], bf16x8g (&bl)[2], int t, int pitch,
+                                       bool next) {
+  auto q0 = [&](int pb) -> int { return (int)((qp[pb >> 1] >> (16 * (pb & 1))) & 0xffffu); };
+  const int toff = (t / KS) * pitch + (t - (t / KS) * KS);
+  const int tn = t + 1;
+  const int toff_n = (tn / KS) * pitch + (tn - (tn / KS) * KS);
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const int cur = pb & 1;
+    if (pb + 1 < NPB) {
+      bh[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + (q0(pb + 1) + toff) * 16);
+      bl[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(pb + 1) + toff) * 16);
+    } else if (next) {
+      bh[NPB & 1] = *(const bf16x8g*)(bp0 + (q0(0) + toff_n) * 16);
+      bl[NPB & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(0) + toff_n) * 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
+      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+    }
+  }
+  if constexpr (NPB & 1) {
+    const bf16x8g th = bh[0], tl = bl[0];
+    bh[0] = bh[1];
+    bl[0] = bl[1];
+    bh[1] = th;
+    bl[1] = tl;
+  }
+}
+
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB, bool RASTER, bool WREG>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                                    SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -125,13 +164,18 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   constexpr int SLOT_W = 4 * PLANE_W;    // one (tap, chunk) weight tile
   constexpr int NWP = 4 * CH / NWAVE;    // 1-KiB weight pieces per wave per tap
   // DB (double-buffered halo, 2 workgroups per CU at <= 80 KiB each) keeps a 2-slot weight ring
-  // RASTER (tiles over the batch's raster order, 2 halo regions) keeps a 4-slot ring for pairs
-  constexpr int RING = PAIR ? (RASTER ? 4 : 6) : (DB ? 2 : 3);
-  constexpr int AHEAD = PAIR ? (RASTER ? 2 : 4) : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
+  // tap pairs use a 4-slot ring (2 taps ahead) where LDS is tight: RASTER (tiles over the batch's
+  // raster order, 2 halo regions) and 3x3 (2 workgroups per CU)
+  constexpr bool RING4 = RASTER || KS == 3;
+  // WREG: no weight ring -- every wave loads its own A fragments from L2 straight into registers,
+  // one tap ahead, so the taps need no workgroup barrier at all (only the halo reload does)
+  constexpr int RING = WREG ? 0 : PAIR ? (RING4 ? 4 : 6) : (DB ? 2 : 3);
+  constexpr int AHEAD = PAIR ? (RING4 ? 2 : 4) : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
   constexpr int CAP = PG * NPB * 32;     // output pixels per tile
   static_assert(NWP >= 1 && NWP <= 2 && PG >= 1, "wave / channel split");
   static_assert(!DB || !PAIR, "double-buffered halo runs one tap per barrier");
   static_assert(!RASTER || (!DB && !POOL), "raster tiles: single halo buffer, plain epilogue");
+  static_assert(!WREG || (!DB && !PAIR), "register weights: one tap at a time, single halo buffer");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
 
   // ---- which tile / weight set ----
@@ -235,8 +279,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[cb][pb][e] = 0.0f;
 
+  if constexpr (!WREG)
 #pragma unroll
-  for (int i = 0; i < AHEAD; ++i) stage_w(i);
+    for (int i = 0; i < AHEAD; ++i) stage_w(i);
   const char* const bp0 = halo + (2 * hi) * hplane;  // this lane's k-half: hi plane, lo plane follows
   const int wlane = (ch * 64 + l32) * 16;
   constexpr int HSTEP = NWAVE / 4;
@@ -300,7 +345,18 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
         big_taps<NPB, KS, PLANE_W>(1, acc, bp, hplane, qp, wb, wb, t, tl.pitch, hi);
       }
     }
-  } else
+  } else {
+  bf16x8g wa_h[2], wa_l[2], wn_h[2], wn_l[2], wb_h[2], wb_l[2];
+  const char* const wl = (const char*)g.w + ((int64_t)co0 + ch * 64 + l32) * 16 + (2 * hi) * wplane;
+  auto load_a = [&](int it2, bf16x8g (&ah)[2], bf16x8g (&al)[2]) {  // WREG: this lane's A fragments of step it2
+    if (it2 >= n_it) it2 = n_it - 1;
+    const char* p = wl + (int64_t)it2 * wstep;
+    ah[0] = *(const bf16x8g*)p;
+    ah[1] = *(const bf16x8g*)(p + 512);
+    al[0] = *(const bf16x8g*)(p + wplane);
+    al[1] = *(const bf16x8g*)(p + wplane + 512);
+  };
+  if constexpr (WREG) load_a(0, wa_h, wa_l);
   for (int c = 0; c < s.c16; ++c) {
     // ---- halo reload; everyone is past the previous chunk's reads ----
     __builtin_amdgcn_s_barrier();
@@ -338,7 +394,20 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (PAIR) {
+    if constexpr (WREG) {
+      wb_h[0] = *(const bf16x8g*)(bp0 + (int)(qp[0] & 0xffffu) * 16);  // block 0 of tap 0
+      wb_l[0] = *(const bf16x8g*)(bp0 + hplane + (int)(qp[0] & 0xffffu) * 16);
+#pragma unroll 1
+      for (int t = 0; t < KSQ; ++t, ++it) {
+        load_a(it + 1, wn_h, wn_l);  // next step's A: lands during this tap's MFMAs
+        wv_tap<NPB, KS>(acc, bp0, hplane, qp, wa_h, wa_l, wb_h, wb_l, t, tl.pitch, t + 1 < KSQ);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          wa_h[cb] = wn_h[cb];
+          wa_l[cb] = wn_l[cb];
+        }
+      }
+    } else if constexpr (PAIR) {
 #pragma unroll 1
       for (int t = 0; t < KSQ; t += 2) {
         // taps (t, t+1) share one barrier: W(it), W(it+1) landed for this wave (W(it+2), W(it+3)
@@ -369,6 +438,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
         big_taps<NPB, KS, PLANE_W>(1, acc, bp0, hplane, qp, wb, wb, t, tl.pitch, hi);
       }
     }
+  }
   }
   wait_vmcnt<0>();  // drain the trailing (never read) weight copies
 
@@ -464,18 +534,24 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
           vl[e] = __builtin_bit_cast(unsigned short, l16);
         }
         char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+#ifdef BIG_NO_STORE  // timing experiment only: epilogue stores skipped unless the value is a NaN
+        if (v[0] != v[0]) {
+#endif
         *(u16x4g*)d = vh;
         *(u16x4g*)(d + 16) = vl;
         if (o32) *(floatx4*)(o32 + co) = v;
+#ifdef BIG_NO_STORE
+        }
+#endif
       }
   }
 }
 
 // ---- host side ----
 struct BigConfig {
-  int ks, npb, nwave, cw, pair, db = 0, raster = 0;
+  int ks, npb, nwave, cw, pair, db = 0, raster = 0, wreg = 0;
   int cap() const { return (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
-  int ring_bytes() const { return (pair ? (raster ? 4 : 6) : (db ? 2 : 3)) * 4 * cw * 16; }
+  int ring_bytes() const { return wreg ? 0 : (pair ? ((raster || ks == 3) ? 4 : 6) : (db ? 2 : 3)) * 4 * cw * 16; }
   int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
   int halo_budget() const { return (lds_budget() - ring_bytes()) / (db ? 2 : 1); }
 };
@@ -546,19 +622,20 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   return true;
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false, bool RASTER = false>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false, bool RASTER = false,
+          bool WREG = false>
 static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
-  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB, RASTER};
+  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB, RASTER, WREG};
   const int lds = k.ring_bytes() + (DB ? 2 : 1) * 4 * tl.nh * 1024;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER, WREG>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER, WREG>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
@@ -636,7 +713,9 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
     *taken = 1;
     return launch_big_t<3, 6, 4, 128, 0, true, true>(s, g, t, st);
   }
-  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, 0} : BigConfig{3, 4, 4, 64, 0};
+  static const int v3 = getenv("OP_BIG3") ? atoi(getenv("OP_BIG3")) : 0;  // tuning aid: 3x3 variant
+  const bool pair = v3 == 3;
+  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, pair} : BigConfig{3, 4, 4, 64, pair};
   t.tc = 32;
   t.tr = k.cap() / 32;  // rows = pixel groups x NPB (even)
   if (halo_bytes(t.tr, t.tc, 3) > k.halo_budget()) return OP_OK;
@@ -650,6 +729,7 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
   t.per_unit = s.n * t.tiles_y * t.tiles_x;
   t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
   *taken = 1;
+  if (pair) return c128 ? launch_big_t<3, 6, 4, 128, 1, true>(s, g, t, st) : launch_big_t<3, 4, 4, 64, 1, true>(s, g, t, st);
   if (c128) return launch_big_t<3, 6, 4, 128, 0, true>(s, g, t, st);
   return launch_big_t<3, 4, 4, 64, 0, true>(s, g, t, st);
 }
@@ -670,6 +750,15 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   BigTiling tl{};
   if (s.ks == 7) {
     if (!c128) return OP_OK;
+    if (s.halo_mode == 10) {  // register weights (no ring, no tap barriers), OP_WV_NPB 5 or 6
+      static const int npb = getenv("OP_WV_NPB") ? atoi(getenv("OP_WV_NPB")) : 5;
+      if (raster_tiling(BigConfig{7, npb == 6 ? 6 : 5, 8, 128, 0, 0, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
+        if (plain_order) tl.xpu = 0;
+        *taken = 1;
+        return npb == 6 ? launch_big_t<7, 6, 8, 128, 0, false, false, true, true>(s, g, tl, st)
+                        : launch_big_t<7, 5, 8, 128, 0, false, false, true, true>(s, g, tl, st);
+      }
+    }
     if (s.halo_mode != 9 && raster_tiling(BigConfig{7, 6, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
       if (plain_order) tl.xpu = 0;
       *taken = 1;
@@ -682,6 +771,13 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   }
   if (c128) {
     static const int v3 = getenv("OP_BIG3") ? atoi(getenv("OP_BIG3")) : 0;  // tuning aid: 3x3 variant
+    if (v3 == 3) {  // 4-wave pairs (2 workgroups per CU, 4-slot ring)
+      const BigConfig k{3, 6, 4, 128, 1};
+      if (!big_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
+      if (plain_order) tl.xpu = 0;
+      *taken = 1;
+      return launch_big_t<3, 6, 4, 128, 1>(s, g, tl, st);
+    }
     if (v3 == 1 || v3 == 2) {
       const BigConfig k{3, 6, 8, 128, v3 == 1 ? 1 : 0};
       if (!big_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;

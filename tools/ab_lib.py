@@ -1,5 +1,6 @@
-"""Interleaved A/B of library builds (OP_LIB_VARIANT) with per-class times: each variant runs in
-its own child process per round (a process loads one library).  usage: ab_lib.py ROUNDS base v1 ..."""
+"""Interleaved A/B of library builds (OP_LIB_VARIANT) or environment settings with per-class times:
+each variant runs in its own child process per round (a process loads one library).
+usage: ab_lib.py ROUNDS base v1 NAME=VALUE[,NAME=VALUE] ...  (an '=' spec sets env vars, product lib)"""
 import json
 import os
 import subprocess
@@ -11,7 +12,10 @@ here = os.path.dirname(os.path.abspath(__file__))
 out = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
-        env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
+        if "=" in v:
+            env = dict(os.environ, OP_LIB_VARIANT="", **dict(kv.split("=", 1) for kv in v.split(",")))
+        else:
+            env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
         p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--steps", "10",
                             "--warmup", "2"], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode:
