@@ -59,7 +59,10 @@ def cpu_baseline(frames, maps, n_frames):
 
 
 KERNEL_7X7 = {0: "conv_bf16x3<7", 1: "conv7_halo_bf16x3", 2: "conv7_halo_bf16x3", 3: "conv_halo_bf16x3<7",
-              4: "conv_big_bf16x3<7", 5: "conv_big_bf16x3<7", 8: "conv_big_bf16x3<7"}
+              4: "conv_m16_bf16x3<7", 5: "conv_m16_bf16x3<7", 6: "conv_pair_bf16x3<7", 7: "conv_db_bf16x3<7",
+              8: "conv_m16_bf16x3<7", 9: "conv_big_bf16x3<7", 10: "conv_big_bf16x3<7", 11: "conv_big_bf16x3<7"}
+MFMA_7X7 = {4: "v_mfma_f32_16x16x32_bf16", 5: "v_mfma_f32_16x16x32_bf16", 6: "v_mfma_f32_16x16x32_bf16",
+            8: "v_mfma_f32_16x16x32_bf16"}
 
 
 def committed_traffic(kernel, batch, precision, halo_mode):
@@ -89,9 +92,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=42,
-                    help="frames per step per GPU (42: the 7x7 kernel's 3 tiles/frame x 2 branches x 42 = 252 "
-                         "workgroups, one per CU)")
+    ap.add_argument("--batch", type=int, default=38,
+                    help="frames per step per GPU (38: the 7x7 kernel's 640-pixel raster tiles, "
+                         "ceil(38 x 2116 / 640) = 126 per branch x 2 = 252 workgroups, one per CU)")
     ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
                     help="post-process input: COCO-like 6-person maps (default) or the random-weight "
                          "network's own last stage")
@@ -197,8 +200,8 @@ def main():
         if args.precision == "bf16x3":
             # 3 bf16 MFMA products per f32-accurate MAC: the f32-accurate peak is 2500/3 TFLOP/s
             peak = BF16_DENSE_PEAK_TFLOPS / 3.0
-            kern = "%s (7x7 stage convs, 3xBF16 split on v_mfma_f32_32x32x16_bf16)" % KERNEL_7X7.get(
-                halo_mode, "conv_bf16x3<7")
+            kern = "%s (7x7 stage convs, 3xBF16 split on %s)" % (
+                KERNEL_7X7.get(halo_mode, "conv_bf16x3<7"), MFMA_7X7.get(halo_mode, "v_mfma_f32_32x32x16_bf16"))
         else:
             peak = FP32_MATRIX_PEAK_TFLOPS
             kern = "conv_mfma_f32<7,2,2> (7x7 stage convs, v_mfma_f32_32x32x2_f32)"

@@ -95,12 +95,13 @@ int op_set_precision(op_ctx* ctx, int32_t mode);
 int op_get_precision(op_ctx* ctx, int32_t* mode);
 
 /* Kernel family of the bf16x3 convolutions (a tuning knob; every family computes the same
- * products, parity-tested): 4 (default) shared-weight halo tiles for 7x7 + 3x3 (conv_big.hip);
- * 5 the same for 7x7 only; 6 the 7x7 on 16x16x32 tap pairs (conv_pair.hip), 3x3 as 4;
+ * products, parity-tested): 4 (default) shared-weight halo tiles (conv_big.hip): the 7x7 layers
+ * on v_mfma_f32_16x16x32_bf16 tap pairs over raster tiles (640-pixel ranges of the batch that
+ * span frame borders), the 3x3 layers on 32x32x16 rectangular tiles; 5 the same for 7x7 only;
+ * 6 the 7x7 on 16x16x32 tap pairs with rectangular tiles (conv_pair.hip), 3x3 as 4;
  * 7 double-buffered 8-channel halos for 7x7 + 3x3 (conv_db.hip); 8 as 4 with the 3x3 c128
- * layers on double-buffered halos (the next 16-channel chunk streams in during this one); 9 as 4
- * with the 7x7 layers on rectangular per-frame tiles instead of raster tiles (768-pixel ranges of
- * the batch that span frame borders, the default wherever their halo fits LDS);
+ * layers on double-buffered halos; 9 / 11 as 4 with the 7x7 on 32x32x16 rectangular / raster
+ * tiles; 10 as 11 with every wave loading its weights into registers (no weight ring);
  * 3 co-split halo tiles (conv_halo.hip); 1 / 2 the 7x7 halo kernel with one / two halo buffers;
  * 0 the per-tap gather kernel.  Shapes a family does not take use the gather kernel. */
 int op_set_conv_algo(op_ctx* ctx, int32_t algo);
