@@ -231,7 +231,7 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     const int rc = launch_conv_pair(s, g, st, &taken);
     if (rc || taken) return rc;
   }
-  if (s.halo_mode == 4 || s.halo_mode == 6 || s.halo_mode == 8 || s.halo_mode == 9 || s.halo_mode == 10 || s.halo_mode == 11 || (s.halo_mode == 5 && s.ks == 7)) {  // conv_big.hip
+  if (s.halo_mode == 4 || s.halo_mode == 6 || s.halo_mode == 8 || s.halo_mode == 9 || s.halo_mode == 10 || s.halo_mode == 11 || s.halo_mode == 12 || (s.halo_mode == 5 && s.ks == 7)) {  // conv_big.hip
     int taken = 0;
     const int rc = launch_conv_big(s, g, st, &taken);
     if (rc || taken) return rc;

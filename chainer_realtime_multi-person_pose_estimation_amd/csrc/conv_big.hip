@@ -748,6 +748,241 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
 }
 
+// ---- 3x3 on v_mfma_f32_16x16x32_bf16 with K = 32 input channels (default 3x3 kernel) ----
+// One step = one tap over a PAIR of 16-channel chunks: lane group g holds k = 8g..8g+7 = chunk
+// g/2 of the pair, channel half g%2.  The halo holds both chunks (8 planes); the weight ring slot
+// holds the tap's weights of both chunks.  Workgroup = 4 waves (2 channel halves x 2 pixel groups,
+// two workgroups per CU at <= 80 KiB), tile = 8 rows x 32 columns; wave = 64 channels x 8 blocks
+// of 16 px (block b = half a tile row).  POOL: fused 2x2 max-pool epilogue (rows = blocks b, b+2).
+template <bool POOL>
+__global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
+                                                           BigTiling tl) {
+  constexpr int KS = 3, KSQ = 9, R = 1;
+  constexpr int CW = 128, PG = 2, NPX = 8;
+  constexpr int PLANE_W = CW * 16;
+  constexpr int CHUNK_W = 4 * PLANE_W;   // one chunk's (tap) weights
+  constexpr int SLOT_W = 2 * CHUNK_W;    // a step: the chunk pair
+  constexpr int RING = 2;
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 2 chunks x 4 planes]
+
+  const int lin = blockIdx.x;
+  int unit, widx;
+  if (tl.xpu) {
+    const int xcd = lin & 7, slot = lin >> 3;
+    unit = xcd / tl.xpu;
+    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
+  } else {
+    unit = lin / tl.per_unit;
+    widx = lin - unit * tl.per_unit;
+  }
+  if (unit >= tl.units || widx >= tl.per_unit) return;
+  const int grp = unit / tl.co_tiles;
+  const int co0 = (unit - grp * tl.co_tiles) * CW;
+  const SplitConvGroup g = grp == 0 ? g0 : g1;
+  if (co0 >= g.cop) return;
+  const int tpf = tl.tiles_y * tl.tiles_x;
+  const int frame = widx / tpf;
+  const int tix = widx - frame * tpf;
+  const int ty = tix / tl.tiles_x;
+  const int y0 = ty * tl.tr, x0 = (tix - ty * tl.tiles_x) * tl.tc;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ch = wave / PG, pg = wave % PG;
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int csel = kg >> 1, khalf = kg & 1;
+  const int hplane = tl.nh * 1024;
+  char* const halo = lds + RING * SLOT_W;
+  const int wp_in = s.w + 2 * s.pin;
+  const int hp_in = s.h + 2 * s.pin;
+  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
+  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
+
+  // weights: 16 1-KiB pieces per step; wave w copies j = 4w .. 4w+3: chunk j/8, plane (j/2)%4, half j%2
+  const int64_t wplane = (int64_t)g.cop * 16;
+  const int64_t wstep = 4 * wplane;  // one (chunk, tap)
+  const int n_it = (s.c16 / 2) * KSQ;
+  auto stage_w = [&](int it) {
+    char* dst = lds + (it % RING) * SLOT_W;
+    if (it >= n_it) it = n_it - 1;
+    const int cp = it / KSQ, t = it - (it / KSQ) * KSQ;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;
+      const int cj = j >> 3, pl = (j >> 1) & 3, hf = j & 1;
+      const char* src = (const char*)g.w + ((int64_t)(2 * cp + cj) * KSQ + t) * wstep + pl * wplane +
+                        ((int64_t)co0 + 64 * hf + lane) * 16;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR_G(dst + cj * CHUNK_W + pl * PLANE_W + hf * 1024), 16,
+                                       0, 0);
+    }
+  };
+
+  const int rows_here = min(tl.tr, s.h - y0);
+  const int cols_here = min(tl.tc, s.w - x0);
+  uint32_t qp[NPX / 2];
+#pragma unroll
+  for (int pb = 0; pb < NPX; ++pb) {
+    const int b = pg * NPX + pb;
+    const int r = b >> 1, c = (b & 1) * 16 + l16;
+    const uint32_t q = (r < rows_here && c < cols_here) ? (uint32_t)(r * tl.pitch + c) : 0u;
+    if (pb & 1) qp[pb >> 1] |= q << 16;
+    else qp[pb >> 1] = q;
+  }
+  auto q0 = [&](int pb) -> int { return (int)((qp[pb >> 1] >> (16 * (pb & 1))) & 0xffffu); };
+
+  floatx4 acc[4][NPX];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  stage_w(0);
+  const char* const bplane = halo + (csel * 4 + 2 * khalf) * hplane;          // hi plane; lo at + hplane
+  const int wlane = csel * CHUNK_W + (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;
+  // halo reload: 8 planes x nh pieces over 4 waves; wave w: planes w and w + 4 (chunk 0 / 1)
+  int it = 0;
+  for (int cp = 0; cp < s.c16 / 2; ++cp) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int cj = 0; cj < 2; ++cj) {
+      const char* src0 = fbase + (2 * cp + cj) * 64 + wave * 16;
+      char* dst = halo + (cj * 4 + wave) * hplane;
+      int hr = lane / tl.pitch, hc = lane - (lane / tl.pitch) * tl.pitch;
+      for (int i = 0; i < tl.nh; ++i) {
+        const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
+                                         16, 0, 0);
+        dst += 1024;
+        hc += 64;
+        while (hc >= tl.pitch) {
+          hc -= tl.pitch;
+          ++hr;
+        }
+      }
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll 1
+    for (int t = 0; t < KSQ; ++t, ++it) {
+      if (t > 0) {
+        wait_vmcnt<0>();  // W(it): the newest copy, issued one step back ...
+        __builtin_amdgcn_s_barrier();  // ... landed for every wave; slot (it+1) % 2 is free
+        asm volatile("" ::: "memory");
+      }
+      stage_w(it + 1);
+      const char* wsl = lds + (it % RING) * SLOT_W + wlane;
+      bf16x8g ah[4], al[4];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
+        al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
+      }
+      const int toff = (t / KS) * tl.pitch + (t - (t / KS) * KS);
+      bf16x8g bh[2], bl[2];
+      bh[0] = *(const bf16x8g*)(bplane + (q0(0) + toff) * 16);
+      bl[0] = *(const bf16x8g*)(bplane + hplane + (q0(0) + toff) * 16);
+#pragma unroll
+      for (int pb = 0; pb < NPX; ++pb) {
+        const int cur = pb & 1;
+        if (pb + 1 < NPX) {
+          bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
+          bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();
+
+  if constexpr (POOL) {
+    // rows (b, b+2) = tile rows (r, r+1); columns (l16, l16 ^ 1) = lanes (l, l ^ 1)
+    const int wp_out = s.w / 2 + 2 * s.pout;
+    const int hp_out = s.h / 2 + 2 * s.pout;
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      if (pb & 2) continue;
+      const int b = pg * NPX + pb;
+      const int r = b >> 1, c = (b & 1) * 16 + l16;
+      const int y = y0 + r, x = x0 + c;
+      const bool store = r < rows_here && c < cols_here && (l16 & 1) == 0;
+      char* optr = (char*)g.out +
+                   ((int64_t)(frame * hp_out + y / 2 + s.pout) * wp_out + (x / 2 + s.pout)) * (int64_t)s.cs_out * 4;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+        const bool live = co < g.cout_store;
+        const floatx4 bv = live ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f};
+        u16x4g vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float m = 0.0f;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            float f = acc[cb][pb + 2 * k][e] + bv[e];
+            if (s.relu) f = f > 0.0f ? f : 0.0f;
+            const __bf16 h16 = (__bf16)f;
+            const float rc = (float)h16 + (float)(__bf16)(f - (float)h16);
+            m = k == 0 ? rc : fmaxf(m, rc);
+          }
+          m = fmaxf(m, __shfl_xor(m, 1));
+          const __bf16 h16 = (__bf16)m;
+          const __bf16 l16v = (__bf16)(m - (float)h16);
+          vh[e] = __builtin_bit_cast(unsigned short, h16);
+          vl[e] = __builtin_bit_cast(unsigned short, l16v);
+        }
+        if (store && live) {
+          char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+          *(u16x4g*)d = vh;
+          *(u16x4g*)(d + 16) = vl;
+        }
+      }
+    }
+    return;
+  }
+
+  const int wp_out = s.w + 2 * s.pout;
+  const int hp_out = s.h + 2 * s.pout;
+#pragma unroll
+  for (int pb = 0; pb < NPX; ++pb) {
+    const int b = pg * NPX + pb;
+    const int r = b >> 1, c = (b & 1) * 16 + l16;
+    if (r >= rows_here || c >= cols_here) continue;
+    const int y = y0 + r, x = x0 + c;
+    char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
+    float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+      if (co >= g.cout_store) continue;
+      const floatx4 bv = *(const floatx4*)(g.bias + co);
+      floatx4 v;
+      u16x4g vh, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float fv = acc[cb][pb][e] + bv[e];
+        if (s.relu) fv = fv > 0.0f ? fv : 0.0f;
+        v[e] = fv;
+        const __bf16 h16 = (__bf16)fv;
+        const __bf16 l16v = (__bf16)(fv - (float)h16);
+        vh[e] = __builtin_bit_cast(unsigned short, h16);
+        vl[e] = __builtin_bit_cast(unsigned short, l16v);
+      }
+      char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+      *(u16x4g*)d = vh;
+      *(u16x4g*)(d + 16) = vl;
+      if (o32) *(floatx4*)(o32 + co) = v;
+    }
+  }
+}
+
 // ---- host side ----
 struct BigConfig {
   int ks, npb, nwave, cw, pair, db = 0, raster = 0, wreg = 0;
@@ -900,6 +1135,52 @@ static bool db_tiling(const SplitConvShape& s, int groups, int cop_max, BigTilin
   return true;
 }
 
+// Default 3x3 c128 layers with c16 even (algos 4, 9-11; 12 keeps conv_big_bf16x3 for them) on
+// conv_m16k_bf16x3 (8 x 32 tiles, 2 workgroups per CU: 32 KiB weight ring + 8-plane halo <= 48
+// KiB; 2-19 % faster per layer than conv_big_bf16x3<3,..> in an interleaved A/B).  false when the
+// shape does not fit (the 46-wide maps, conv1_2's 64 channels).
+static bool m16k_tiling(const SplitConvShape& s, int groups, int cop_max, bool pool, BigTiling& t) {
+  const int m = s.halo_mode;
+  if ((m != 4 && m != 9 && m != 10 && m != 11) || s.ks != 3 || cop_max % 128 || (s.c16 & 1) || s.pin < 1)
+    return false;
+  t.tc = 32;
+  t.tr = 8;
+  t.tiles_x = (s.w + 31) / 32;
+  t.tiles_y = (s.h + 7) / 8;
+  if (!pool && (double)s.w / (t.tiles_x * 32) < 0.9) return false;  // narrow maps: conv_big
+  t.pitch = halo_pitch(32, 3);
+  t.hrows = 10;
+  t.nh = (t.hrows * t.pitch + 63) / 64;
+  if (2 * 2 * 4 * 128 * 16 + 8 * t.nh * 1024 > 80 * 1024) return false;
+  t.co_tiles = (cop_max + 127) / 128;
+  t.units = groups * t.co_tiles;
+  t.per_unit = s.n * t.tiles_y * t.tiles_x;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  return true;
+}
+
+static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, bool pool, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16k_bf16x3<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     80 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16k_bf16x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     80 * 1024));
+    attr = true;
+  }
+  const int lds = 2 * 2 * 4 * 128 * 16 + 8 * tl.nh * 1024;
+  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+                                 : (unsigned)(tl.units * tl.per_unit);
+  const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+  if (pool)
+    hipLaunchKernelGGL(conv_m16k_bf16x3<true>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+  else
+    hipLaunchKernelGGL(conv_m16k_bf16x3<false>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+  OP_AFTER_LAUNCH("conv_m16k_bf16x3", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 // 3x3 conv + ReLU + 2x2 max-pool in one launch: s.h x s.w is the conv size, the output buffer is
 // (s.h/2) x (s.w/2) with halo s.pout.  Tiles are 32 columns x (pixel groups x NPB) rows.
 // *taken = 0 when the shape is outside this kernel (the caller runs conv + pool).
@@ -910,6 +1191,10 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
     return OP_OK;
   const bool c128 = g[0].cop % 128 == 0;
   BigTiling t{};
+  if (c128 && m16k_tiling(s, 1, g[0].cop, true, t)) {
+    *taken = 1;
+    return launch_m16k(s, g, t, true, st);
+  }
   if (c128 && db_tiling(s, 1, g[0].cop, t)) {
     *taken = 1;
     return launch_big_t<3, 6, 4, 128, 0, true, true>(s, g, t, st);
@@ -1004,6 +1289,11 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       return v3 == 1 ? launch_big_t<3, 6, 8, 128, 1>(s, g, tl, st) : launch_big_t<3, 6, 8, 128, 0>(s, g, tl, st);
+    }
+    if (m16k_tiling(s, s.groups, cop_max, false, tl)) {
+      if (plain_order) tl.xpu = 0;
+      *taken = 1;
+      return launch_m16k(s, g, tl, false, st);
     }
     if (db_tiling(s, s.groups, cop_max, tl)) {
       if (plain_order) tl.xpu = 0;

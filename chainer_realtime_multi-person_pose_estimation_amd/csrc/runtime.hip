@@ -1769,8 +1769,8 @@ int op_set_precision(op_ctx* c, int32_t mode) {
 int op_set_conv_algo(op_ctx* c, int32_t algo) {
   using namespace op;
   RC(check_ctx(c, false));
-  if (algo < 0 || algo > 11) {
-    set_error("conv algo must be 0..11");
+  if (algo < 0 || algo > 12) {
+    set_error("conv algo must be 0..12");
     return OP_ERR_INVALID;
   }
   c->conv_algo = algo;

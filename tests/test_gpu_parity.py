@@ -125,7 +125,7 @@ def test_forward_368_vs_oracle(precision_ctx, rand_weights):
     _fwd_check(precision_ctx, rand_weights, x)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("algo", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_conv_algos_agree(ctx, algo):
     """Every bf16x3 kernel family computes the same forward (batch 2 at 368x368 and 720p-shaped
     656x368) as the default family, within the 3xBF16 rounding (the default is held to the oracle
