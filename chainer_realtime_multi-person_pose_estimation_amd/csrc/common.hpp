@@ -94,6 +94,24 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
 int launch_conv_db(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, bool pool, int* taken);
 // 7x7 tap-pair kernel on v_mfma_f32_16x16x32_bf16 (conv_pair.hip)
 int launch_conv_pair(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
+// fused 1x1 pair at the end of a branch (conv_head.hip): in -> W1 (ReLU) -> W2 (no ReLU) -> out
+struct HeadGroup {
+  const float* in;       // split NHWC input, offset by the group's first input channel
+  const void* w1;        // split weights of the first 1x1 [c16][plane][cop1][8]
+  const float* b1;
+  int32_t cop1;
+  const void* w2;        // split weights of the second 1x1 [c16][plane][cop2][8]
+  const float* b2;
+  int32_t cop2;
+  float* out;            // split NHWC output, offset by the group's first output channel
+  int32_t cout_store;    // channels written (multiple of 4, <= 48)
+  float* out32;          // optional dense f32 copy (n*h*w, cs_out32), or null
+  int32_t out32_off;
+};
+struct HeadShape {
+  int32_t n, h, w, pin, cs_in, pout, cs_out, ci, co1, groups, cs_out32;
+};
+int launch_conv_head(const HeadShape& s, const HeadGroup* g, hipStream_t st, int* taken);
 int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
                           int32_t c, hipStream_t st);
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);

@@ -1,0 +1,238 @@
+// Fused 1x1 pair at the end of every branch (3xBF16 split, gfx950): conv5_4 + conv5_5
+// (CocoPoseNet.py:157-158, 162-163: 128 -> 512 ReLU -> 38 | 19) and Mconv6 + Mconv7 of stages
+// 2-6 (e.g. :174-175, 181-182: 128 -> 128 ReLU -> 38 | 19).
+//
+// The intermediate (512 or 128 channels per pixel) never reaches HBM: a workgroup owns 64
+// consecutive pixels of the batch (raster order, crossing frame borders) of one branch.
+//  * its input tile (64 px x Ci split channels) is copied once into LDS;
+//  * for each 128-channel chunk of the intermediate, GEMM1 (v_mfma_f32_16x16x32_bf16, K = 32
+//    input channels per step, products hi*hi + hi*lo + lo*hi) -> + bias, ReLU, hi/lo split ->
+//    LDS, then GEMM2 accumulates that chunk's contribution to the <= 48 output channels in
+//    registers;
+//  * the epilogue adds the second bias and writes the split output (and the dense f32 copy of
+//    the last stage's maps) straight into the stage-input (concat) buffer slices.
+// Waves: 4; GEMM1: wave w = intermediate blocks 2w, 2w+1 (16 ch each) x 4 pixel blocks;
+// GEMM2: wave w = pixel block w x all output blocks.  Weights come from L2 (the CU's tiles share
+// them), issued a K step (GEMM2) or a chunk (GEMM1) ahead.  Mconv6+7 (one chunk): the intermediate
+// overwrites the input tile, 33 KiB LDS, 4 workgroups per CU; conv5_4+5 (4 chunks): 67.5 KiB, 2.
+#include "common.hpp"
+
+namespace op {
+
+typedef __bf16 bf16x8h __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4h __attribute__((ext_vector_type(4)));
+
+constexpr int kHeadPx = 64;
+
+__device__ __forceinline__ floatx4 mfma3(const bf16x8h& ah, const bf16x8h& al, const bf16x8h& bh, const bf16x8h& bl,
+                                        floatx4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  return acc;
+}
+
+template <int NB2, bool ONE>
+__global__ __launch_bounds__(256, ONE ? 4 : 2) void conv_head_bf16x3(HeadShape s, HeadGroup g0, HeadGroup g1, int32_t per_group) {
+  constexpr int CI = 128;  // both pairs read 128 channels per branch
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int grp = blockIdx.x >= (unsigned)per_group ? 1 : 0;
+  const HeadGroup g = grp ? g1 : g0;
+  const int P0 = (blockIdx.x - grp * per_group) * kHeadPx;
+  const int hw = s.h * s.w;
+  const int total = s.n * hw;
+  constexpr int xpitch = CI * 4 + 16;  // +16 B: consecutive pixels start 4 banks apart
+  constexpr int tpitch = 128 * 4 + 16;
+  char* const X = lds;
+  char* const T = ONE ? lds : lds + kHeadPx * xpitch;  // ONE (co1 = 128): T overwrites X after GEMM1
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int wp_in = s.w + 2 * s.pin, hp_in = s.h + 2 * s.pin;
+
+  const int64_t wpl1 = (int64_t)g.cop1 * 16;  // bytes per (c16, plane) of W1
+  const int64_t wpl2 = (int64_t)g.cop2 * 16;
+  const char* const w1 = (const char*)g.w1;
+  const char* const w2 = (const char*)g.w2;
+  const int kh = kg & 1;
+  // A fragments of GEMM1 for one chunk: 4 K steps x 2 channel blocks x (hi, lo), issued ahead
+  bf16x8h a1[4][2][2];
+  auto load_a1 = [&](int chunk) {
+    const int co_a = chunk + wave * 32 + l16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c16 = 2 * k + (kg >> 1);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const char* wa = w1 + (int64_t)(c16 * 4 + 2 * kh) * wpl1 + (int64_t)(co_a + 16 * cb) * 16;
+        a1[k][cb][0] = *(const bf16x8h*)wa;
+        a1[k][cb][1] = *(const bf16x8h*)(wa + wpl1);
+      }
+    }
+  };
+  load_a1(0);
+  // ---- input tile -> LDS (16-B pieces; pixels past the batch repeat the last one) ----
+  {
+    constexpr int pieces = CI / 4;
+    for (int i = threadIdx.x; i < kHeadPx * pieces; i += 256) {
+      const int px = i / pieces, pc = i - px * pieces;
+      const int P = min(P0 + px, total - 1);
+      const int f = P / hw, pp = P - f * hw;
+      const int y = pp / s.w, x = pp - y * s.w;
+      const float* src = g.in + ((int64_t)(f * hp_in + y + s.pin) * wp_in + x + s.pin) * s.cs_in + pc * 4;
+      *(uint4*)(X + px * xpitch + pc * 16) = *(const uint4*)src;
+    }
+  }
+  __syncthreads();
+
+  floatx4 acc2[NB2];
+#pragma unroll
+  for (int j = 0; j < NB2; ++j) acc2[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int chunk = 0; chunk < (ONE ? 128 : s.co1); chunk += 128) {
+    // ---- GEMM1: intermediate channels chunk + 32w .. +31 x 64 px ----
+    floatx4 acc1[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) acc1[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const char* xb = X + (pb * 16 + l16) * xpitch + (4 * k + kg) * 32;
+        const bf16x8h bh = *(const bf16x8h*)xb;
+        const bf16x8h bl = *(const bf16x8h*)(xb + 16);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc1[cb][pb] = mfma3(a1[k][cb][0], a1[k][cb][1], bh, bl, acc1[cb][pb]);
+      }
+    }
+    // GEMM2's A fragments of the first K step, in flight across the T write and barrier
+    bf16x8h a2[NB2][2];
+    auto load_a2 = [&](int k) {
+      const int c16 = chunk / 16 + 2 * k + (kg >> 1);
+#pragma unroll
+      for (int j = 0; j < NB2; ++j) {
+        const char* wa = w2 + (int64_t)(c16 * 4 + 2 * kh) * wpl2 + (int64_t)(j * 16 + l16) * 16;
+        a2[j][0] = *(const bf16x8h*)wa;
+        a2[j][1] = *(const bf16x8h*)(wa + wpl2);
+      }
+    };
+    load_a2(0);
+    if constexpr (ONE) __syncthreads();  // every wave is done with X before T overwrites it
+    // ---- bias + ReLU + split -> T[px][chunk channel] ----
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int cl = wave * 32 + cb * 16 + 4 * kg;  // chunk-relative channel of e = 0
+      const floatx4 bv = *(const floatx4*)(g.b1 + chunk + cl);
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        u16x4h vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc1[cb][pb][e] + bv[e];
+          v = v > 0.0f ? v : 0.0f;
+          const __bf16 h16 = (__bf16)v;
+          const __bf16 l16v = (__bf16)(v - (float)h16);
+          vh[e] = __builtin_bit_cast(unsigned short, h16);
+          vl[e] = __builtin_bit_cast(unsigned short, l16v);
+        }
+        char* d = T + (pb * 16 + l16) * tpitch + (cl >> 3) * 32 + (cl & 7) * 2;
+        *(u16x4h*)d = vh;
+        *(u16x4h*)(d + 16) = vl;
+      }
+    }
+    __syncthreads();
+    // ---- GEMM2: pixel block `wave` x NB2 output blocks, K = this chunk ----
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const char* tb = T + (wave * 16 + l16) * tpitch + (4 * k + kg) * 32;
+      const bf16x8h bh = *(const bf16x8h*)tb;
+      const bf16x8h bl = *(const bf16x8h*)(tb + 16);
+      bf16x8h cur[NB2][2];
+#pragma unroll
+      for (int j = 0; j < NB2; ++j) {
+        cur[j][0] = a2[j][0];
+        cur[j][1] = a2[j][1];
+      }
+      if (k + 1 < 4) load_a2(k + 1);
+#pragma unroll
+      for (int j = 0; j < NB2; ++j) acc2[j] = mfma3(cur[j][0], cur[j][1], bh, bl, acc2[j]);
+    }
+    // next chunk's GEMM1 fragments: issued after GEMM2's (vmcnt retires in order)
+    if (!ONE && chunk + 128 < s.co1) load_a1(chunk + 128);
+    __syncthreads();  // T is rewritten by the next chunk
+  }
+
+  // ---- epilogue: + bias2 (no ReLU), split store into the concat slice (+ dense f32 copy) ----
+  const int P = P0 + wave * 16 + l16;
+  if (P >= total) return;
+  const int f = P / hw, pp = P - f * hw;
+  const int y = pp / s.w, x = pp - y * s.w;
+  const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
+  char* const optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + x + s.pout) * (int64_t)s.cs_out * 4;
+  float* const o32 = g.out32 ? g.out32 + (int64_t)P * s.cs_out32 + g.out32_off : nullptr;
+#pragma unroll
+  for (int j = 0; j < NB2; ++j) {
+    const int co = j * 16 + 4 * kg;
+    if (co >= g.cout_store) continue;
+    const floatx4 bv = *(const floatx4*)(g.b2 + co);
+    floatx4 v;
+    u16x4h vh, vl;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float fv = acc2[j][e] + bv[e];
+      v[e] = fv;
+      const __bf16 h16 = (__bf16)fv;
+      const __bf16 l16v = (__bf16)(fv - (float)h16);
+      vh[e] = __builtin_bit_cast(unsigned short, h16);
+      vl[e] = __builtin_bit_cast(unsigned short, l16v);
+    }
+    char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+    *(u16x4h*)d = vh;
+    *(u16x4h*)(d + 16) = vl;
+    if (o32) *(floatx4*)(o32 + co) = v;
+  }
+}
+
+template <int NB2>
+static int launch_head_t(const HeadShape& s, const HeadGroup* g, hipStream_t st) {
+  const int total = s.n * s.h * s.w;
+  const int per = (total + kHeadPx - 1) / kHeadPx;
+  const bool one = s.co1 == 128;
+  const int lds = kHeadPx * (128 * 4 + 16) * (one ? 1 : 2);
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  if (one)
+    hipLaunchKernelGGL((conv_head_bf16x3<NB2, true>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s, g[0],
+                       s.groups > 1 ? g[1] : g[0], per);
+  else
+    hipLaunchKernelGGL((conv_head_bf16x3<NB2, false>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s, g[0],
+                     s.groups > 1 ? g[1] : g[0], per);
+  OP_AFTER_LAUNCH("conv_head_bf16x3", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// *taken = 0 when the shape is outside this kernel (the caller runs the two 1x1 convs).
+int launch_conv_head(const HeadShape& s, const HeadGroup* g, hipStream_t st, int* taken) {
+  *taken = 0;
+  if (s.ci != 128 || s.co1 % 128 || s.cs_in % 8 || s.groups < 1 || s.groups > 2) return OP_OK;
+  int store = 0;
+  for (int i = 0; i < s.groups; ++i) {
+    if (g[i].cop1 < s.co1 || g[i].cout_store % 4 || g[i].cout_store > 48 || g[i].cop2 < g[i].cout_store) return OP_OK;
+    store = store > g[i].cout_store ? store : g[i].cout_store;
+  }
+  *taken = 1;
+  if (store > 32) return launch_head_t<3>(s, g, st);
+  if (store > 16) return launch_head_t<2>(s, g, st);
+  return launch_head_t<1>(s, g, st);
+}
+
+}  // namespace op

@@ -487,6 +487,14 @@ struct HeatFull {  // already-upsampled planes [f*18 + j][mh][mw]
   }
 };
 
+// Early out of a tile: every value the NMS sees is a convex combination of the tile's source
+// values (bilinear f32 weights >= 0 summing to 1 within 4 ulp, normalised non-negative Gaussian taps
+// in f64, two f32 roundings), so it is <= M + |M| * 1e-6 for the source maximum M.  A tile whose
+// sources all stay below thresh - |.| * 1e-4 cannot hold a value > thresh, hence no peak.
+__device__ __forceinline__ bool may_reach(float v, float thresh) {
+  return (double)v + fabs((double)v) * 1e-4 >= (double)thresh;
+}
+
 // R > 0: radius fixed at compile time (register-blocked passes, NV outputs per thread); R == 0: any
 // radius <= kMaxR given at run time (one output per thread).
 template <class Src, int R>
@@ -530,12 +538,17 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
     const LowMap m = low_map(src.src, src.lw, f);
     const int c = src.src.heat_off + j;
     float* win = tmp;
+    bool live = !staged;
     if (staged)
       for (int i = threadIdx.x; i < nwy * nwx; i += kFN) {
         const int a = i / nwx;
-        win[i] = m.at(c, wy + a, wx + (i - a * nwx));
+        const float v = m.at(c, wy + a, wx + (i - a * nwx));
+        win[i] = v;
+        live |= may_reach(v, thresh);
       }
-    __syncthreads();
+    // No low-res value of the window can lift the upsampled + smoothed tile above the peak
+    // threshold: the tile has no peak, skip the passes (result identical, see may_reach).
+    if (!__syncthreads_or(live)) return;
     for (int i = threadIdx.x; i < ur * uc; i += kFN) {
       const int ly = i / uc, lx = i - ly * uc;
       const UpTap t = up_tap2(rt[ly], ct[lx]);
@@ -549,10 +562,14 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
       up[ly * kFU + lx] = v;
     }
   } else {
+    bool live = false;
     for (int i = threadIdx.x; i < ur * uc; i += kFN) {
       const int ly = i / uc, lx = i - ly * uc;
-      up[ly * kFU + lx] = src.at(f, j, reflect_near(uy0 + ly, mh), reflect_near(ux0 + lx, mw));
+      const float v = src.at(f, j, reflect_near(uy0 + ly, mh), reflect_near(ux0 + lx, mw));
+      up[ly * kFU + lx] = v;
+      live |= may_reach(v, thresh);
     }
+    if (!__syncthreads_or(live)) return;
   }
   __syncthreads();
   if constexpr (R > 0) {

@@ -651,6 +651,50 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
     if (_r) return _r;   \
   } while (0)
 
+// Fused 1x1 pair per branch (conv5_4+conv5_5, Mconv6+Mconv7): in -> a (ReLU) -> b -> out, the
+// intermediate kept on chip (conv_head.hip).  Returns -1 when not taken (the caller then runs the
+// two convs through `mid`).  OP_HEAD_FUSED=0 disables it (A/B).
+static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1,
+                 const PackedConv* a, const PackedConv* b, int st0, int st1, const Act* out32, int o32a, int o32b) {
+  static const bool off = getenv("OP_HEAD_FUSED") && atoi(getenv("OP_HEAD_FUSED")) == 0;
+  if (!c->split || off) return -1;
+  HeadShape s;
+  s.n = c->gn;
+  s.h = out.h;
+  s.w = out.w;
+  s.pin = in.pad;
+  s.cs_in = in.cs;
+  s.pout = out.pad;
+  s.cs_out = out.cs;
+  s.ci = a[0].cin16;
+  s.co1 = a[0].cop;
+  s.groups = 2;
+  s.cs_out32 = out32 ? out32->cs : 0;
+  HeadGroup g[2];
+  const int cis[2] = {ci0, ci1}, cos[2] = {co0, co1}, sts[2] = {st0, st1}, o32[2] = {o32a, o32b};
+  for (int i = 0; i < 2; ++i) {
+    g[i].in = in.p + cis[i];
+    g[i].w1 = a[i].ws;
+    g[i].b1 = a[i].b;
+    g[i].cop1 = a[i].cop;
+    g[i].w2 = b[i].ws;
+    g[i].b2 = b[i].b;
+    g[i].cop2 = b[i].cop;
+    g[i].out = out.p + cos[i];
+    g[i].cout_store = sts[i];
+    g[i].out32 = out32 ? out32->p : nullptr;
+    g[i].out32_off = o32[i];
+  }
+  double fl = 0, by = 0;
+  for (int i = 0; i < 2; ++i) {
+    conv_work(c, out, a[i], &fl, &by);
+    conv_work(c, out, b[i], &fl, &by);
+  }
+  int taken = 0;
+  const int rc = profiled(c, 2, fl, by, [&] { return launch_conv_head(s, g, c->stream, &taken); });
+  return rc ? rc : (taken ? 0 : -1);
+}
+
 static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
   if (c->split) return launch_maxpool2_split(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
   return launch_maxpool2(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
@@ -689,8 +733,15 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   RC(conv1(c, cat, kCatFeat, B[B_BRA], 0, c->s1_first, 256, true));
   RC(conv2(c, B[B_BRA], 0, 128, B[B_BRB], 0, 128, c->s1_g[0][0], c->s1_g[1][0], 128, 128, true));
   RC(conv2(c, B[B_BRB], 0, 128, B[B_BRA], 0, 128, c->s1_g[0][1], c->s1_g[1][1], 128, 128, true));
-  RC(conv2(c, B[B_BRA], 0, 128, s1, 0, 512, c->s1_g[0][2], c->s1_g[1][2], 512, 512, true));
-  RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false));
+  {
+    const PackedConv a[2] = {c->s1_g[0][2], c->s1_g[1][2]}, b[2] = {c->s1_last[0], c->s1_last[1]};
+    const int h = head2(c, B[B_BRA], 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, nullptr, 0, 0);
+    if (h > 0) return h;
+    if (h < 0) {
+      RC(conv2(c, B[B_BRA], 0, 128, s1, 0, 512, c->s1_g[0][2], c->s1_g[1][2], 512, 512, true));
+      RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false));
+    }
+  }
   // stages 2-6 (CocoPoseNet.py:167-260)
   Act s6 = B[B_S1];
   s6.cs = 256;  // Mconv6 output reuses the stage-1 1x1 buffer (no halo) with a 256-channel stride
@@ -702,10 +753,16 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
       RC(conv2(c, *src, 0, 128, *dst, 0, 128, c->st_g[st][0][i], c->st_g[st][1][i], 128, 128, true));
       std::swap(src, dst);
     }
-    RC(conv2(c, *src, 0, 128, s6, 0, 128, c->st_g[st][0][4], c->st_g[st][1][4], 128, 128, true));
     // the last stage also leaves a dense f32 copy (paf at 0, heat at 40) for the post-process
-    RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false,
-             (c->split && st == 4) ? &B[B_MAP32] : nullptr, 0, 40));
+    const Act* m32 = (c->split && st == 4) ? &B[B_MAP32] : nullptr;
+    const PackedConv a[2] = {c->st_g[st][0][4], c->st_g[st][1][4]}, b[2] = {c->st_last[st][0], c->st_last[st][1]};
+    const int h = head2(c, *src, 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
+    if (h > 0) return h;
+    if (h < 0) {
+      RC(conv2(c, *src, 0, 128, s6, 0, 128, c->st_g[st][0][4], c->st_g[st][1][4], 128, 128, true));
+      RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false, m32, 0,
+               40));
+    }
   }
   return OP_OK;
 }
