@@ -133,6 +133,11 @@ int launch_conv11_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_
                         const float* x0, int32_t n, int32_t h, int32_t w, const float* wt, const float* bias,
                         float* out, hipStream_t st);
 
+// conv1_1 + conv1_2 + 2x2 max-pool fused (conv1_pair.hip); frames as for launch_conv11_split
+int launch_conv1_pair(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t sh, int32_t sw,
+                      const float* x0, int32_t n, int32_t h, int32_t w, const float* wt11, const float* b11,
+                      const void* w12, const float* b12, float* out, int32_t pout, hipStream_t st);
+
 // ---- multi-scale path (precise.hip) ----
 int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
                             int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);

@@ -1,0 +1,259 @@
+// conv1_1 + conv1_2 + 2x2 max-pool in one launch (CocoPoseNet.py:136-138), 3xBF16 split, gfx950.
+//
+// conv1_1 (3 -> 64, K = 27) is VALU work; conv1_2 (64 -> 64) is MFMA work.  Run separately, the
+// 64-channel conv1_1 map (1.4 GB split at 38 frames of 368x368) is written once and read ~2x by
+// conv1_2.  Here a workgroup owns an 8 x 32 tile of conv1_2 outputs (4 x 16 pooled) and:
+//  * stages the 12 x 36 network-input window (cv2 LINEAR resize + x/255 - 0.5 from the uint8
+//    frame, pose_detector.py:493-494, 426-431, or the padded split16 input) in LDS;
+//  * per 32-channel half of conv1_1: computes conv1_1 + bias + ReLU on the 10 x 34 window conv1_2
+//    reads (zero outside the image: conv1_2's own zero padding), in the same FMA order as
+//    conv11_split, and writes it hi/lo split into 8 LDS planes (chunk x k-half x hi/lo);
+//  * runs conv1_2's 9 taps of that half on v_mfma_f32_16x16x32_bf16 (K = 32 channels: lane group
+//    g = chunk g/2, channel half g%2; products hi*hi + hi*lo + lo*hi), A fragments read from L2
+//    one step ahead;
+//  * pools 2x2 in the epilogue (rows = blocks b, b+2; columns = lanes l, l^1) into P1.
+// Waves: 4, wave w = 64 channels x the tile's rows 2w, 2w+1 (4 blocks of 16 px).  LDS 48 KiB:
+// three workgroups per CU, so one's conv1_1 (VALU) phase overlaps the others' MFMA phases.
+#include "common.hpp"
+#include "cvlinear.hpp"
+
+namespace op {
+
+typedef __bf16 bf16x8p __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4p __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8p __attribute__((ext_vector_type(8)));
+
+constexpr int kP1R = 8, kP1C = 32;                 // conv1_2 tile
+constexpr int kP1HR = kP1R + 2, kP1HC = kP1C + 2;  // conv1_1 window = conv1_2 halo (pitch kP1HC)
+constexpr int kP1IR = kP1R + 4, kP1IC = kP1C + 4;  // network-input window
+constexpr int kP1Slots = kP1HR * kP1HC;            // 340
+constexpr int kP1Plane = kP1Slots * 16;            // bytes per plane
+constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
+
+__device__ __forceinline__ float p1_recon(float v) {
+  const __bf16 h = (__bf16)v;
+  return (float)h + (float)(__bf16)(v - (float)h);
+}
+
+template <bool FROM_FRAMES>
+__global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __restrict__ frames, int64_t frame_bytes,
+                                                            int64_t row_stride, int sh, int sw,
+                                                            const char* __restrict__ x0in, int h, int w,
+                                                            const float* __restrict__ wt11,
+                                                            const float* __restrict__ b11, const char* __restrict__ w12,
+                                                            const float* __restrict__ b12, char* __restrict__ out,
+                                                            int pout) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const halo = lds;                           // 8 planes x 340 slots x 16 B
+  float* const inw = (float*)(lds + 8 * kP1Plane);  // [3][12][36] f32, planar: lanes read consecutive words
+  const int n = blockIdx.z;
+  const int y0 = blockIdx.y * kP1R, x0 = blockIdx.x * kP1C;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int csel = kg >> 1, khalf = kg & 1;
+
+  // ---- network-input window (zero outside the image: conv1_1's padding) ----
+  for (int i = tid; i < kP1IR * kP1IC; i += 256) {
+    const int iy = i / kP1IC, ix = i - (i / kP1IC) * kP1IC;
+    const int gy = y0 - 2 + iy, gx = x0 - 2 + ix;
+    float v[3] = {0.f, 0.f, 0.f};
+    if (gy >= 0 && gy < h && gx >= 0 && gx < w) {
+      if constexpr (FROM_FRAMES) {
+        const uint8_t* src = frames + (int64_t)n * frame_bytes;
+        const LinTap tx = cv_linear_tap(gx, w, sw, true);
+        const LinTap ty = cv_linear_tap(gy, h, sh, false);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = p1_recon(cv_linear_px(src, row_stride, sh, sw, tx, ty, c));
+      } else {  // padded split16 input (h+2, w+2, 16): channels 0..7 hi at +0, lo at +16
+        const char* p = x0in + (((int64_t)n * (h + 2) + gy + 1) * (w + 2) + gx + 1) * 64;
+        const uint2 hv = *(const uint2*)p, lv = *(const uint2*)(p + 16);
+        v[0] = __fadd_rn(__uint_as_float(hv.x << 16), __uint_as_float(lv.x << 16));
+        v[1] = __fadd_rn(__uint_as_float(hv.x & 0xffff0000u), __uint_as_float(lv.x & 0xffff0000u));
+        v[2] = __fadd_rn(__uint_as_float(hv.y << 16), __uint_as_float(lv.y << 16));
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) inw[c * kP1IR * kP1IC + i] = v[c];
+  }
+
+  // A fragments (conv1_2 weights, split layout [c16][tap][plane][64][8]) of step (half, tap)
+  auto load_a = [&](int half, int t, bf16x8p(&ah)[4], bf16x8p(&al)[4]) {
+    const int c16 = 2 * half + csel;
+    const char* base = w12 + ((int64_t)((c16 * 9 + t) * 4 + 2 * khalf) * 64 + l16) * 16;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      ah[cb] = *(const bf16x8p*)(base + cb * 256);
+      al[cb] = *(const bf16x8p*)(base + 64 * 16 + cb * 256);
+    }
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // this lane's halo slot for its 4 pixel blocks (block b = 4w + pb: row b/2, cols (b%2)*16 + l16)
+  int q[4];
+#pragma unroll
+  for (int pb = 0; pb < 4; ++pb) {
+    const int b = 4 * wave + pb;
+    q[pb] = (b >> 1) * kP1HC + (b & 1) * 16 + l16;
+  }
+  const char* const bplane = halo + (csel * 4 + 2 * khalf) * kP1Plane;
+
+  bf16x8p ah[4], al[4];
+  load_a(0, 0, ah, al);
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // input window staged / the previous half's MFMAs are done with the halo
+    // ---- conv1_1 for channels 32*half .. +31 on the 10 x 34 window -> split LDS planes ----
+    for (int it = tid; it < 2 * kP1Items; it += 256) {
+      // 16-channel group within the half: wave-uniform (kP1Items is a multiple of 64), so the
+      // weights are scalar operands as in conv11_split
+      const int grp = __builtin_amdgcn_readfirstlane(it / kP1Items);
+      const int s = it - grp * kP1Items;
+      if (s >= kP1Slots) continue;
+      const int ry = s / kP1HC, rx = s - (s / kP1HC) * kP1HC;
+      const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
+      const int cbase = 32 * half + 16 * grp;
+      u16x8p hv[2], lv[2];
+      if (gy >= 0 && gy < h && gx >= 0 && gx < w) {
+        float a[16];
+#pragma unroll
+        for (int co = 0; co < 16; ++co) a[co] = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float* px = inw + (ry + t / 3) * kP1IC + rx + t % 3;
+#pragma unroll
+          for (int ci = 0; ci < 3; ++ci) {
+            const float v = px[ci * kP1IR * kP1IC];
+#pragma unroll
+            for (int co = 0; co < 16; ++co) a[co] = __fmaf_rn(v, wt11[(t * 3 + ci) * 64 + cbase + co], a[co]);
+          }
+        }
+#pragma unroll
+        for (int co = 0; co < 16; ++co) {
+          float f = __fadd_rn(a[co], b11[cbase + co]);
+          f = f > 0.0f ? f : 0.0f;
+          const __bf16 hh = (__bf16)f;
+          const __bf16 ll = (__bf16)(f - (float)hh);
+          hv[co >> 3][co & 7] = __builtin_bit_cast(unsigned short, hh);
+          lv[co >> 3][co & 7] = __builtin_bit_cast(unsigned short, ll);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          hv[k] = u16x8p{0, 0, 0, 0, 0, 0, 0, 0};
+          lv[k] = u16x8p{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
+      // planes: chunk grp, k-half k, hi / lo
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        *(u16x8p*)(halo + (grp * 4 + 2 * k) * kP1Plane + s * 16) = hv[k];
+        *(u16x8p*)(halo + (grp * 4 + 2 * k + 1) * kP1Plane + s * 16) = lv[k];
+      }
+    }
+    __syncthreads();
+    // ---- conv1_2, the 9 taps of this half: K = 32 channels per step ----
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      bf16x8p ch_[4], cl_[4];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        ch_[cb] = ah[cb];
+        cl_[cb] = al[cb];
+      }
+      if (t + 1 < 9) load_a(half, t + 1, ah, al);
+      else if (half == 0) load_a(1, 0, ah, al);
+      const int toff = (t / 3) * kP1HC + t % 3;
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const char* bp = bplane + (q[pb] + toff) * 16;
+        const bf16x8p bh = *(const bf16x8p*)bp;
+        const bf16x8p bl = *(const bf16x8p*)(bp + kP1Plane);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ch_[cb], bh, acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ch_[cb], bl, acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cl_[cb], bh, acc[cb][pb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: + bias, ReLU, split round trip, 2x2 max-pool -> P1 (pad pout, 64 channels) ----
+  const int wp_out = w / 2 + 2 * pout;
+  const int hp_out = h / 2 + 2 * pout;
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {  // blocks pb (row 2w) and pb + 2 (row 2w + 1)
+    const int b = 4 * wave + pb;
+    const int r = b >> 1, c = (b & 1) * 16 + l16;
+    const int y = y0 + r, x = x0 + c;
+    const bool store = y < h && x < w && (l16 & 1) == 0;
+    char* optr = out + ((int64_t)(n * hp_out + y / 2 + pout) * wp_out + (x / 2 + pout)) * 256;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int co = cb * 16 + 4 * kg;
+      const floatx4 bv = *(const floatx4*)(b12 + co);
+      u16x4p vh, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float m = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          float f = acc[cb][pb + 2 * k][e] + bv[e];
+          f = f > 0.0f ? f : 0.0f;
+          const __bf16 h16 = (__bf16)f;
+          const float rc = (float)h16 + (float)(__bf16)(f - (float)h16);
+          m = k == 0 ? rc : fmaxf(m, rc);
+        }
+        m = fmaxf(m, __shfl_xor(m, 1));
+        const __bf16 h16 = (__bf16)m;
+        const __bf16 l16v = (__bf16)(m - (float)h16);
+        vh[e] = __builtin_bit_cast(unsigned short, h16);
+        vl[e] = __builtin_bit_cast(unsigned short, l16v);
+      }
+      if (store) {
+        char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+        *(u16x4p*)d = vh;
+        *(u16x4p*)(d + 16) = vl;
+      }
+    }
+  }
+}
+
+// conv1_1 + conv1_2 + pool: frames != nullptr reads the uint8 frames (sh x sw resized to h x w),
+// else the padded split16 network input x0.  wt11: conv1_1 [tap][ci][co] f32; w12: conv1_2 split
+// weights (cop 64); out: P1 (h/2 + 2 pout, w/2 + 2 pout, 64) split.
+int launch_conv1_pair(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t sh, int32_t sw,
+                      const float* x0, int32_t n, int32_t h, int32_t w, const float* wt11, const float* b11,
+                      const void* w12, const float* b12, float* out, int32_t pout, hipStream_t st) {
+  if (h % 2 || w % 2) {
+    set_error("conv1_pair: odd map size");
+    return OP_ERR_INVALID;
+  }
+  const int lds = 8 * kP1Plane + kP1IR * kP1IC * 12;
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv1_pair_bf16x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv1_pair_bf16x3<false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const dim3 grid((unsigned)((w + kP1C - 1) / kP1C), (unsigned)((h + kP1R - 1) / kP1R), (unsigned)n);
+  if (frames)
+    hipLaunchKernelGGL(conv1_pair_bf16x3<true>, grid, dim3(256), lds, st, frames, frame_bytes, row_stride, sh, sw,
+                       nullptr, h, w, wt11, b11, (const char*)w12, b12, (char*)out, pout);
+  else
+    hipLaunchKernelGGL(conv1_pair_bf16x3<false>, grid, dim3(256), lds, st, nullptr, 0, 0, 0, 0, (const char*)x0, h, w,
+                       wt11, b11, (const char*)w12, b12, (char*)out, pout);
+  OP_AFTER_LAUNCH("conv1_pair_bf16x3", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+}  // namespace op

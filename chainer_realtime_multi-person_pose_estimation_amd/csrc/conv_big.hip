@@ -647,6 +647,9 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   for (int c = 0; c < s.c16; ++c) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef M16_SKIP_RELOAD  // timing experiment only (wrong results): halo loaded for chunk 0 only
+    if (c == 0)
+#endif
     {
       const char* src0 = fbase + c * 64 + h_plane * 16;
       const char* src0_b = fbase_b + c * 64 + h_plane * 16;
@@ -669,17 +672,22 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    bf16x8g ah[4], al[4];
 #pragma unroll 1
     for (int t = 0; t < KSQ; t += 2) {
+#ifndef M16_NO_BARRIER  // timing experiment only (races on the weight ring)
       wait_vmcnt<0>();  // W(it), W(it+1): the newest copies, issued one pair back ...
       __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
       asm volatile("" ::: "memory");
+#endif
       stage_w(it + 2);
       stage_w(it + 3);
       const bool two = t + 1 < KSQ;
       const int tt = two ? t + tsel : t;  // the odd last tap: upper k groups get zero weights
       const char* wsl = lds + ((two ? it + tsel : it) % RING) * SLOT_W + wlane;
-      bf16x8g ah[4], al[4];
+#ifdef M16_ONE_AREAD  // timing experiment only (wrong results): A fragments read once per chunk
+      if (t == 0)
+#endif
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
@@ -696,10 +704,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
         const int cur = pb & 1;
+#ifndef M16_ONE_BREAD  // timing experiment only (wrong results): one B fragment per tap pair
         if (pb + 1 < NPX) {
           bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
           bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
         }
+#else
+        bh[cur ^ 1] = bh[cur];
+        bl[cur ^ 1] = bl[cur];
+#endif
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
@@ -754,11 +767,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 // holds the tap's weights of both chunks.  Workgroup = 4 waves (2 channel halves x 2 pixel groups,
 // two workgroups per CU at <= 80 KiB), tile = 8 rows x 32 columns; wave = 64 channels x 8 blocks
 // of 16 px (block b = half a tile row).  POOL: fused 2x2 max-pool epilogue (rows = blocks b, b+2).
-template <bool POOL>
+// TCB = 16-pixel blocks per tile row: 2 (8 x 32 tiles, NPX 8) or 3 (4 x 48 tiles, NPX 6: the 46- and
+// 82-wide maps, where 32-column tiles leave 28 % / 15 % of the MFMA lanes on padding).
+template <bool POOL, int TCB = 2, int NPX = 8>
 __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                            BigTiling tl) {
+  static_assert(!POOL || TCB == 2, "the pooled epilogue pairs blocks b, b + 2");
+  static_assert((2 * NPX) % TCB == 0, "whole tile rows");
   constexpr int KS = 3, KSQ = 9, R = 1;
-  constexpr int CW = 128, PG = 2, NPX = 8;
+  constexpr int CW = 128, PG = 2;
   constexpr int PLANE_W = CW * 16;
   constexpr int CHUNK_W = 4 * PLANE_W;   // one chunk's (tap) weights
   constexpr int SLOT_W = 2 * CHUNK_W;    // a step: the chunk pair
@@ -823,7 +840,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
     const int b = pg * NPX + pb;
-    const int r = b >> 1, c = (b & 1) * 16 + l16;
+    const int r = b / TCB, c = (b % TCB) * 16 + l16;
     const uint32_t q = (r < rows_here && c < cols_here) ? (uint32_t)(r * tl.pitch + c) : 0u;
     if (pb & 1) qp[pb >> 1] |= q << 16;
     else qp[pb >> 1] = q;
@@ -953,7 +970,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
     const int b = pg * NPX + pb;
-    const int r = b >> 1, c = (b & 1) * 16 + l16;
+    const int r = b / TCB, c = (b % TCB) * 16 + l16;
     if (r >= rows_here || c >= cols_here) continue;
     const int y = y0 + r, x = x0 + c;
     char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
@@ -1143,13 +1160,18 @@ static bool m16k_tiling(const SplitConvShape& s, int groups, int cop_max, bool p
   const int m = s.halo_mode;
   if ((m != 4 && m != 9 && m != 10 && m != 11) || s.ks != 3 || cop_max % 128 || (s.c16 & 1) || s.pin < 1)
     return false;
-  t.tc = 32;
-  t.tr = 8;
-  t.tiles_x = (s.w + 31) / 32;
-  t.tiles_y = (s.h + 7) / 8;
-  if (!pool && (double)s.w / (t.tiles_x * 32) < 0.9) return false;  // narrow maps: conv_big
-  t.pitch = halo_pitch(32, 3);
-  t.hrows = 10;
+  static const bool no48 = getenv("OP_M16K_NO48") && atoi(getenv("OP_M16K_NO48")) != 0;  // A/B aid
+  // 8 x 32 tiles, or 4 x 48 where they waste fewer MFMA lanes (narrow maps; not with the pool)
+  const double u32 = (double)s.w / (((s.w + 31) / 32) * 32) * s.h / (((s.h + 7) / 8) * 8);
+  const double u48 = (double)s.w / (((s.w + 47) / 48) * 48) * s.h / (((s.h + 3) / 4) * 4);
+  const bool w48 = !pool && !no48 && u48 > u32 + 0.02;
+  t.tc = w48 ? 48 : 32;
+  t.tr = w48 ? 4 : 8;
+  t.tiles_x = (s.w + t.tc - 1) / t.tc;
+  t.tiles_y = (s.h + t.tr - 1) / t.tr;
+  if (!pool && !w48 && (double)s.w / (t.tiles_x * 32) < 0.9) return false;  // narrow maps: conv_big
+  t.pitch = t.tc + 2;  // 16-px blocks never wrap a tile row: tight pitch
+  t.hrows = t.tr + 2;
   t.nh = (t.hrows * t.pitch + 63) / 64;
   if (2 * 2 * 4 * 128 * 16 + 8 * t.nh * 1024 > 80 * 1024) return false;
   t.co_tiles = (cop_max + 127) / 128;
@@ -1166,6 +1188,8 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
                                      80 * 1024));
     OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16k_bf16x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      80 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16k_bf16x3<false, 3, 6>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
     attr = true;
   }
   const int lds = 2 * 2 * 4 * 128 * 16 + 8 * tl.nh * 1024;
@@ -1174,6 +1198,8 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
   if (pool)
     hipLaunchKernelGGL(conv_m16k_bf16x3<true>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+  else if (tl.tc == 48)
+    hipLaunchKernelGGL((conv_m16k_bf16x3<false, 3, 6>), dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
   else
     hipLaunchKernelGGL(conv_m16k_bf16x3<false>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
   OP_AFTER_LAUNCH("conv_m16k_bf16x3", st);

@@ -705,7 +705,20 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
                        int sh = 0, int sw = 0) {
   Act* B = c->buf;
   static const bool c11_mfma = getenv("OP_CONV11_MFMA") != nullptr;  // debugging aid: the MFMA conv1_1
-  if (c->split && !(c11_mfma && !frames)) {
+  // conv1_1 + conv1_2 + pool in one launch (conv1_pair.hip); OP_CONV1_FUSED=0: the two-kernel path
+  static const bool c1_fused = !(getenv("OP_CONV1_FUSED") && atoi(getenv("OP_CONV1_FUSED")) == 0);
+  bool conv1_done = false;
+  if (c->split && c1_fused && !c11_mfma && c->conv_algo == 4) {
+    const Act& o = B[B_C11];
+    double fl = 0, by = 0;
+    conv_work(c, o, c->bb[0], &fl, &by);
+    conv_work(c, o, c->bb[1], &fl, &by);
+    RC(profiled(c, conv_class(3), fl, by, [&] {
+      return launch_conv1_pair(frames, frame_bytes, row_stride, sh, sw, B[B_X0].p, c->gn, o.h, o.w, c->w11,
+                               c->bb[0].b, c->bb[1].ws, c->bb[1].b, B[B_P1].p, B[B_P1].pad, c->stream);
+    }));
+    conv1_done = true;
+  } else if (c->split && !(c11_mfma && !frames)) {
     const Act& o = B[B_C11];
     double fl = 0, by = 0;
     conv_work(c, o, c->bb[0], &fl, &by);
@@ -716,7 +729,7 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   } else {
     RC(conv1(c, B[B_X0], 0, B[B_C11], 0, c->bb[0], 64, true));
   }
-  RC(conv_pool(c, B[B_C11], B[B_C12], B[B_P1], c->bb[1], 64));
+  if (!conv1_done) RC(conv_pool(c, B[B_C11], B[B_C12], B[B_P1], c->bb[1], 64));
   RC(conv1(c, B[B_P1], 0, B[B_C21], 0, c->bb[2], 128, true));
   RC(conv_pool(c, B[B_C21], B[B_C22], B[B_P2], c->bb[3], 128));
   RC(conv1(c, B[B_P2], 0, B[B_C3A], 0, c->bb[4], 256, true));

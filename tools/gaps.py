@@ -7,7 +7,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "conv11" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "conv11" in r["Kernel_Name"] or "conv1_pair" in r["Kernel_Name"]]
 i0, i1 = starts[-2], starts[-1]
 step = rows[i0:i1]
 span = (int(step[-1]["End_Timestamp"]) - int(step[0]["Start_Timestamp"])) / 1e3
