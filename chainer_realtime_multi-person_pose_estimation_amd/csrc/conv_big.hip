@@ -47,6 +47,8 @@ struct BigTiling {
   int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
   int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
   int32_t hw, total;         // raster tiles: pixels per frame, pixels of the batch
+  int32_t per_xcd;           // > 0: pixel-major XCD order (conv_m16k): XCD x runs pixel tiles
+                             // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
 };
 
 template <int N>
@@ -556,7 +558,11 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 // 64 channels (4 blocks of 16) x NPX 16-pixel blocks of a raster tile; D rows are channels (4
 // consecutive per lane), columns pixels.  Halo, 4-slot weight ring (one barrier per tap pair, 2
 // taps ahead) and XCD-aware block order as conv_big_bf16x3<7,..,RASTER>.
-template <int KS, int NPX>
+// PF (OP_M16_PF=1): the next tap pair's A fragments and first B fragment are read in the last
+// pixel block of the current pair, each A register right after its last MFMA (no extra VGPRs), so
+// no pair starts on an LDS round trip; the ring barrier moves to the middle of the pair (ring
+// holds 2 pairs: pair p+2 is staged into pair p's slot once every wave holds A(p) in registers).
+template <int KS, int NPX, bool PF = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -643,6 +649,109 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
+  if constexpr (PF) {
+    static_assert(NPX % 2 == 0, "block 0 of the next pair lands in bh[0]");
+    constexpr int NPAIR = (KSQ + 1) / 2;
+    constexpr int MID = NPX / 2;
+    const int n_pairs = s.c16 * NPAIR;
+    // pair p = (chunk p / NPAIR, taps 2j, 2j+1) -> ring pair slot p & 1 (2 tap slots); the odd
+    // last tap reloads itself into the second slot (its A is zeroed) to keep 2 copies per pair
+    auto stage_pair = [&](int p) {
+      char* dst = lds + (p & 1) * 2 * SLOT_W + wdst;
+      if (p >= n_pairs) p = n_pairs - 1;
+      const int c = p / NPAIR, j = p - (p / NPAIR) * NPAIR;
+      const int ia = c * KSQ + 2 * j;
+      const int ib = 2 * j + 1 < KSQ ? ia + 1 : ia;
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)ia * wstep), LDS_PTR_G(dst), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)ib * wstep), LDS_PTR_G(dst + SLOT_W), 16, 0, 0);
+    };
+    auto tap_off = [&](int j) -> int {
+      const int tt = 2 * j + 1 < KSQ ? 2 * j + tsel : 2 * j;
+      return (tt / KS) * tl.pitch + (tt - (tt / KS) * KS);
+    };
+    bf16x8g ah[4], al[4], bh[2], bl[2];
+    auto read_a = [&](int p, int cb) {
+      const int j = p - (p / NPAIR) * NPAIR;
+      const char* wsl = lds + (p & 1) * 2 * SLOT_W + tsel * SLOT_W + wlane;
+      ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
+      al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
+      if (2 * j + 1 >= KSQ && tsel) {
+        ah[cb] = bf16x8g{};
+        al[cb] = bf16x8g{};
+      }
+    };
+    stage_pair(1);  // stage_w(0), stage_w(1) above filled tap slots 0, 1 = pair 0
+    int p = 0;
+    for (int c = 0; c < s.c16; ++c) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      {
+        const char* src0 = fbase + c * 64 + h_plane * 16;
+        const char* src0_b = fbase_b + c * 64 + h_plane * 16;
+        int hr = h_r0, hc = h_c0;
+        char* dst = halo + h_plane * hplane + h_i0 * 1024;
+        for (int i = h_i0; i < tl.nh; i += 2) {
+          const bool in_a = hr < rowsA;
+          const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
+          const int xx = min(hc - R + s.pin, wp_in - 1);
+          __builtin_amdgcn_global_load_lds(
+              (const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst), 16, 0, 0);
+          dst += 2 * 1024;
+          hc += 2 * 64;
+          while (hc >= tl.pitch) {
+            hc -= tl.pitch;
+            ++hr;
+          }
+        }
+      }
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (c == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) read_a(0, cb);
+      }
+      {
+        const int toff = tap_off(0);
+        bh[0] = *(const bf16x8g*)(bplane + (q0(0) + toff) * 16);
+        bl[0] = *(const bf16x8g*)(bplane + hplane + (q0(0) + toff) * 16);
+      }
+#pragma unroll 1
+      for (int j = 0; j < NPAIR; ++j, ++p) {
+        const int toff = tap_off(j);
+#pragma unroll
+        for (int pb = 0; pb < NPX; ++pb) {
+          const int cur = pb & 1;
+          if (pb == MID) {
+            wait_vmcnt<0>();  // pair p+1's copies (staged at the middle of pair p-1) landed ...
+            __builtin_amdgcn_s_barrier();  // ... for every wave; every wave holds A(p): its slot is free
+            asm volatile("" ::: "memory");
+            stage_pair(p + 2);
+          }
+          if (pb + 1 < NPX) {
+            bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
+            bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
+          } else if (j + 1 < NPAIR) {  // block 0 of the next pair (same halo)
+            const int tn = tap_off(j + 1);
+            bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(0) + tn) * 16);
+            bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(0) + tn) * 16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+            if (pb == NPX - 1 && p + 1 < n_pairs) {
+              __builtin_amdgcn_sched_barrier(0);
+              read_a(p + 1, cb);  // A(p+1) landed at this pair's barrier; A(p)[cb] is dead
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      }
+    }
+  } else {
   int it = 0;
   for (int c = 0; c < s.c16; ++c) {
     __builtin_amdgcn_s_barrier();
@@ -724,6 +833,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       it += two ? 2 : 1;
     }
   }
+  }
   wait_vmcnt<0>();
 
   const int wp_out = s.w + 2 * s.pout;
@@ -784,7 +894,12 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 
   const int lin = blockIdx.x;
   int unit, widx;
-  if (tl.xpu) {
+  if (tl.per_xcd) {  // the weight sets of one pixel tile run side by side on one XCD: its input
+    const int xcd = lin & 7, slot = lin >> 3;  // tile is fetched from HBM once, then from L2
+    const int wl = slot / tl.units;
+    unit = slot - wl * tl.units;
+    widx = wl < tl.per_xcd ? xcd * tl.per_xcd + wl : tl.per_unit;
+  } else if (tl.xpu) {
     const int xcd = lin & 7, slot = lin >> 3;
     unit = xcd / tl.xpu;
     widx = slot * tl.xpu + (xcd - unit * tl.xpu);
@@ -1178,6 +1293,14 @@ static bool m16k_tiling(const SplitConvShape& s, int groups, int cop_max, bool p
   t.units = groups * t.co_tiles;
   t.per_unit = s.n * t.tiles_y * t.tiles_x;
   t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  // pixel-major XCD order when several weight sets share the input and all of them fit an XCD's
+  // 4 MiB L2 beside the streamed halos (OP_M16K_PMAJ: 1 when they fit, 2 always; default off: no
+  // gain in an interleaved A/B, the MALL already serves the second read)
+  static const int pmaj = getenv("OP_M16K_PMAJ") ? atoi(getenv("OP_M16K_PMAJ")) : 0;
+  const double wset = (double)s.c16 * 16 * 9 * 128 * 4;  // one weight set, split bf16 bytes
+  t.per_xcd = 0;
+  if (groups == 1 && t.co_tiles > 1 && (pmaj == 2 || (pmaj == 1 && t.units * wset <= 3.0 * 1024 * 1024)))
+    t.per_xcd = (t.per_unit + 7) / 8;
   return true;
 }
 
@@ -1193,8 +1316,9 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
     attr = true;
   }
   const int lds = 2 * 2 * 4 * 128 * 16 + 8 * tl.nh * 1024;
-  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
-                                 : (unsigned)(tl.units * tl.per_unit);
+  const unsigned blocks = tl.per_xcd ? 8u * (unsigned)(tl.per_xcd * tl.units)
+                          : tl.xpu   ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+                                     : (unsigned)(tl.units * tl.per_unit);
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
   if (pool)
     hipLaunchKernelGGL(conv_m16k_bf16x3<true>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
@@ -1268,15 +1392,22 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       static bool attr = false;
+      static const bool pf = getenv("OP_M16_PF") && atoi(getenv("OP_M16_PF")) != 0;
       if (!attr) {
         OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 10>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024));
+        OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 10, true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
       const int lds = 4 * 4 * 128 * 16 + 4 * tl.nh * 1024;
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
-      hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), dim3(blocks), dim3(512), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], tl);
+      if (pf)
+        hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), dim3(blocks), dim3(512), lds, st, s, g[0],
+                           s.groups > 1 ? g[1] : g[0], tl);
+      else
+        hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), dim3(blocks), dim3(512), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], tl);
       OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
       OP_HIP_CHECK(hipGetLastError());
       return OP_OK;
