@@ -110,11 +110,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # OP_BENCH_BACKEND=gloo (rehearsal only: N ranks sharing the GPUs of a smaller box, CPU-side
+    # collectives); the product path is RCCL ('nccl'), one rank per GPU
+    backend = os.environ.get("OP_BENCH_BACKEND", "nccl")
+    coll_dev = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            coll_dev = torch.device("cuda", local)
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            dist.init_process_group(backend)
     import importlib
     L = importlib.import_module(PKG + "._lib")
     Wm = importlib.import_module(PKG + ".weights")
@@ -138,8 +147,9 @@ def main():
     def barrier():
         if dist is not None:
             import torch
-            dist.all_reduce(torch.zeros(1, device="cuda"))
-            torch.cuda.synchronize()
+            dist.all_reduce(torch.zeros(1, device=coll_dev))
+            if coll_dev is not None:
+                torch.cuda.synchronize()
 
     persons = 0
 
@@ -154,7 +164,7 @@ def main():
             import torch
             recs = Fr.pack_records([(rank + world * i, r[2].status, r[2].n_peaks, r[0], r[1])
                                     for i, r in enumerate(res)], 64)
-            Fr.gather_records(recs, 64, device=torch.device("cuda", local))
+            Fr.gather_records(recs, 64, device=coll_dev)
 
     for _ in range(args.warmup):
         step(False)
@@ -184,10 +194,10 @@ def main():
     ctx.profile(False)
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        pt = torch.tensor([float(persons)], device="cuda", dtype=torch.float64)
+        pt = torch.tensor([float(persons)], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(pt)
         persons = float(pt.item())
 
