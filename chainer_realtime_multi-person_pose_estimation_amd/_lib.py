@@ -26,7 +26,10 @@ EXPORTED = (
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_profile_classes",
+    "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
+    "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect",
 )
+ARCH = {"facenet": 1, "handnet": 2}
 MAX_SCALES = 8
 PRECISION = {"fp32": 0, "bf16x3": 1}
 
@@ -103,6 +106,14 @@ def lib():
         "op_set_precision": ([P, I32], ctypes.c_int),
         "op_get_precision": ([P, P], ctypes.c_int),
         "op_fetch_results": ([P, I32, I32, P, P, I32, P], ctypes.c_int),
+        "op_cpm_layer_count": ([I32], ctypes.c_int),
+        "op_cpm_layer_info": ([I32, I32, ctypes.POINTER(ctypes.c_char_p), P, P, P], ctypes.c_int),
+        "op_cpm_create": ([I32, I32, P], ctypes.c_int),
+        "op_cpm_destroy": ([P], ctypes.c_int),
+        "op_cpm_set_weights": ([P, P, P], ctypes.c_int),
+        "op_cpm_forward": ([P, P, I32, I32, I32, P], ctypes.c_int),
+        "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
+        "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -414,3 +425,87 @@ class Context(object):
                                         ctypes.byref(by)), "op_profile_read")
             out[name] = (ms.value, n.value, fl.value, by.value)
         return out
+
+
+def cpm_layer_table(arch):
+    """[(name, ci, co, k)] of FaceNet / HandNet (models/FaceNet.py:11-76) from the library."""
+    a = ARCH[arch]
+    out = []
+    name = ctypes.c_char_p()
+    ci, co, k = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    for i in range(lib().op_cpm_layer_count(a)):
+        check(lib().op_cpm_layer_info(a, i, ctypes.byref(name), ctypes.byref(ci), ctypes.byref(co), ctypes.byref(k)))
+        out.append((name.value.decode(), ci.value, co.value, k.value))
+    return out
+
+
+class CpmContext(object):
+    """Owns one op_cpm_ctx: a FaceNet or HandNet replica on one device (face/hand detectors)."""
+
+    def __init__(self, arch, device=0):
+        if arch not in ARCH:
+            raise ValueError("arch must be one of %s" % sorted(ARCH))
+        self.arch = arch
+        self.table = cpm_layer_table(arch)
+        self.n_maps = self.table[-1][2]
+        h = ctypes.c_void_p()
+        check(lib().op_cpm_create(ARCH[arch], int(device), ctypes.byref(h)), "op_cpm_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().op_cpm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_weights(self, weights):
+        """weights: {layer: (W (Co,Ci,k,k), b (Co,))} for every layer of the table."""
+        Ws, bs = [], []
+        for name, ci, co, k in self.table:
+            W, b = weights[name]
+            W = np.ascontiguousarray(W, np.float32)
+            b = np.ascontiguousarray(b, np.float32)
+            if W.shape != (co, ci, k, k) or b.shape != (co,):
+                raise ValueError("%s: expected W %s b %s, got %s %s" % (name, (co, ci, k, k), (co,), W.shape, b.shape))
+            Ws.append(W)
+            bs.append(b)
+        self._keep = (Ws, bs)
+        Wp = (ctypes.c_void_p * len(Ws))(*[w.ctypes.data for w in Ws])
+        bp = (ctypes.c_void_p * len(bs))(*[v.ctypes.data for v in bs])
+        check(lib().op_cpm_set_weights(self.h, Wp, bp), "op_cpm_set_weights")
+
+    def forward(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        n, _, h, w = x.shape
+        out = np.empty((n, self.n_maps, h // 8, w // 8), np.float32)
+        check(lib().op_cpm_forward(self.h, ptr(x), n, h, w, ptr(out)), "op_cpm_forward")
+        return out
+
+    @staticmethod
+    def _keypoints(kp, found):
+        return [[int(k[0]), int(k[1]), np.float32(k[2])] if f else None for k, f in zip(kp, found)]
+
+    def peaks(self, heatmaps, thresh, flip=False):
+        hm = np.ascontiguousarray(heatmaps, np.float32)
+        c, h, w = hm.shape
+        kp = np.zeros((max(c - 1, 0), 3), np.float64)
+        found = np.zeros(max(c - 1, 0), np.int32)
+        check(lib().op_cpm_peaks(self.h, ptr(hm), c, h, w, float(thresh), int(bool(flip)), ptr(kp), ptr(found)),
+              "op_cpm_peaks")
+        return self._keypoints(kp, found)
+
+    def detect(self, bgr, thresh, flip_maps=False):
+        img = np.ascontiguousarray(bgr, np.uint8)
+        if img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        h, w = img.shape[:2]
+        kp = np.zeros((self.n_maps - 1, 3), np.float64)
+        found = np.zeros(self.n_maps - 1, np.int32)
+        check(lib().op_cpm_detect(self.h, ptr(img), h, w, w * 3, float(thresh), int(bool(flip_maps)), ptr(kp),
+                                  ptr(found)), "op_cpm_detect")
+        return self._keypoints(kp, found)

@@ -116,7 +116,7 @@ int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout
                           int32_t c, hipStream_t st);
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);
 int launch_preprocess_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t n, int32_t sh,
-                            int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st);
+                            int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st, float div = 255.0f);
 int launch_extract_maps32(const float* m, int32_t cs, int32_t heat_off, int32_t n, int32_t h, int32_t w, float* paf,
                           float* heat, hipStream_t st);
 int launch_maxpool2(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,

@@ -573,7 +573,7 @@ int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int
 
 __global__ __launch_bounds__(256) void preprocess_split16(const uint8_t* __restrict__ frames, int64_t frame_bytes,
                                                           int64_t row_stride, int n, int sh, int sw, int dh, int dw,
-                                                          char* __restrict__ out) {
+                                                          char* __restrict__ out, float div) {
   const int wp = dw + 2, hp = dh + 2;
   const int64_t total = (int64_t)n * hp * wp;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -585,17 +585,17 @@ __global__ __launch_bounds__(256) void preprocess_split16(const uint8_t* __restr
   const int dy = py - 1, dx = px - 1;
   if (dy >= 0 && dy < dh && dx >= 0 && dx < dw) {
     const uint8_t* src = frames + (int64_t)nn * frame_bytes;
-    for (int c = 0; c < 3; ++c) v[c] = cv_linear_norm(src, row_stride, sh, sw, dx, dy, dw, dh, c);
+    for (int c = 0; c < 3; ++c) v[c] = cv_linear_norm(src, row_stride, sh, sw, dx, dy, dw, dh, c, div);
   }
   store_split8(out + i * 64, v);
   store_split8(out + i * 64 + 32, z);
 }
 
 int launch_preprocess_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t n, int32_t sh,
-                            int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st) {
+                            int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st, float div) {
   const int64_t total = (int64_t)n * (dh + 2) * (dw + 2);
   hipLaunchKernelGGL(preprocess_split16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, frames, frame_bytes,
-                     row_stride, n, sh, sw, dh, dw, (char*)out);
+                     row_stride, n, sh, sw, dh, dw, (char*)out, div);
   OP_AFTER_LAUNCH("preprocess_split16", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;

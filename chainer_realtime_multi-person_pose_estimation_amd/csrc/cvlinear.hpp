@@ -39,8 +39,9 @@ __device__ __forceinline__ LinTap cv_linear_tap(int d, int dsize, int ssize, boo
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// div: 255 (pose_detector.py:426-431) or 256 (face_detector.py:33, hand_detector.py:36)
 __device__ __forceinline__ float cv_linear_px(const uint8_t* src, int64_t row_stride, int sh, int sw, const LinTap& tx,
-                                              const LinTap& ty, int ch) {
+                                              const LinTap& ty, int ch, float div = 255.0f) {
   const int x0 = tx.s0, x1 = tx.s1 < sw ? tx.s1 : sw - 1;
   const int r0 = clampi(ty.s0, 0, sh - 1), r1 = clampi(ty.s1, 0, sh - 1);
   const uint8_t* p0 = src + (int64_t)r0 * row_stride;
@@ -49,15 +50,15 @@ __device__ __forceinline__ float cv_linear_px(const uint8_t* src, int64_t row_st
   const int h1 = (int)p1[x0 * 3 + ch] * tx.c0 + (int)p1[x1 * 3 + ch] * tx.c1;
   int v = ((((h0 >> 4) * ty.c0) >> 16) + (((h1 >> 4) * ty.c1) >> 16) + 2) >> 2;
   v = clampi(v, 0, 255);
-  return __fsub_rn(__fdiv_rn((float)v, 255.0f), 0.5f);
+  return __fsub_rn(__fdiv_rn((float)v, div), 0.5f);
 }
 
 
 __device__ __forceinline__ float cv_linear_norm(const uint8_t* src, int64_t row_stride, int sh, int sw, int dx, int dy,
-                                                int dw, int dh, int ch) {
+                                                int dw, int dh, int ch, float div = 255.0f) {
   const LinTap tx = cv_linear_tap(dx, dw, sw, true);
   const LinTap ty = cv_linear_tap(dy, dh, sh, false);
-  return cv_linear_px(src, row_stride, sh, sw, tx, ty, ch);
+  return cv_linear_px(src, row_stride, sh, sw, tx, ty, ch, div);
 }
 
 }  // namespace op

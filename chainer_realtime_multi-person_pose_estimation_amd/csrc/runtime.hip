@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "host_pack.hpp"
 
 namespace op {
 
@@ -180,42 +181,11 @@ static void pack_into(std::vector<float>& dst, std::vector<float>& bias, int cop
   (void)c8;
 }
 
-static inline uint16_t bf16_rne(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);  // inf / nan: truncate
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-static inline float bf16_f(uint16_t b) {
-  const uint32_t u = (uint32_t)b << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-
-// Pack Chainer W (Co, Ci, k, k) into the split layout at output-channel offset co_off:
-// element (c16, tap, co, h, part, j) = part 0: bf16(w), part 1: bf16(w - hi) for input channel 16*c16 + 8h + j.
+// Pack Chainer W (Co, Ci, k, k) into the split layout at output-channel offset co_off (host_pack.hpp);
+// cat_input: physical channels of the 192-channel stage input (cat_logical).
 static void pack_split_into(std::vector<uint16_t>& dst, int cop, int cin16, int k, const float* W, int Co, int Ci,
                             int co_off, bool cat_input) {
-  const int taps = k * k;
-  for (int co = 0; co < Co; ++co)
-    for (int p = 0; p < cin16; ++p) {
-      const int ci = cat_input ? cat_logical(p) : (p < Ci ? p : -1);
-      if (ci < 0) continue;
-      const int c16 = p / 16, h = (p % 16) / 8, j = p % 8;
-      for (int t = 0; t < taps; ++t) {
-        const int ky = t / k, kx = t % k;
-        const float v = W[(((size_t)co * Ci + ci) * k + ky) * k + kx];
-        const uint16_t hb = bf16_rne(v);
-        const uint16_t lb = bf16_rne(v - bf16_f(hb));
-        // planar: [c16][tap][plane = 2h + (0 hi | 1 lo)][cop][8]
-        const size_t tile = ((size_t)c16 * taps + t) * 4;
-        dst[((tile + 2 * h) * cop + (co_off + co)) * 8 + j] = hb;
-        dst[((tile + 2 * h + 1) * cop + (co_off + co)) * 8 + j] = lb;
-      }
-    }
+  pack_split(dst, cop, cin16, k, W, Co, Ci, co_off, [&](int p) { return cat_input ? cat_logical(p) : (p < Ci ? p : -1); });
 }
 
 static int upload(PackedConv& pc, const std::vector<float>& w, const std::vector<float>& b) {
@@ -974,31 +944,7 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
   if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
   if (const char* e = getenv("OP_GUARD")) op::g_guard = ((size_t)atol(e) + 255) / 256 * 256;
   // scipy _gaussian_kernel1d(sigma, 0, int(4*sigma + 0.5)) taps (restated; pinned by the tests)
-  {
-    const double sigma = c->prm.gaussian_sigma;
-    const int r = (int)(4.0 * sigma + 0.5);
-    std::vector<double> w(2 * r + 1);
-    const double coef = -0.5 / (sigma * sigma);
-    for (int i = 0; i <= 2 * r; ++i) w[i] = std::exp(coef * (double)((i - r) * (i - r)));
-    // numpy pairwise sum
-    const int n = 2 * r + 1;
-    double s;
-    if (n < 8) {
-      s = 0;
-      for (int i = 0; i < n; ++i) s += w[i];
-    } else {
-      double rr[8];
-      for (int j = 0; j < 8; ++j) rr[j] = w[j];
-      int i = 8;
-      for (; i < n - (n % 8); i += 8)
-        for (int j = 0; j < 8; ++j) rr[j] += w[i + j];
-      s = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
-      for (; i < n; ++i) s += w[i];
-    }
-    for (auto& v : w) v = v / s;
-    c->gauss_host = w;
-    c->gauss_r = r;
-  }
+  c->gauss_r = op::gaussian_taps(c->prm.gaussian_sigma, c->gauss_host);
   *out = c;
   return OP_OK;
 }

@@ -147,3 +147,96 @@ class PoseDetector(object):
         if res.n_persons == 0:
             return np.array([]), np.empty(0)
         return poses, scores
+
+    # ---- crops for the face / hand detectors (pose_detector.py:266-425, host-side, used by demo.py) ----
+    def compute_limbs_length(self, joints):
+        """pose_detector.py:266-276 (joint rows are arrays, never None: every limb gets a length)."""
+        limbs = []
+        limbs_len = np.zeros(len(params["limbs_point"]))
+        for i, (a, b) in enumerate(params["limbs_point"]):
+            if joints[a] is not None and joints[b] is not None:
+                limbs.append([joints[a], joints[b]])
+                limbs_len[i] = np.linalg.norm(joints[b][:-1] - joints[a][:-1])
+            else:
+                limbs.append(None)
+        return limbs_len, limbs
+
+    def compute_unit_length(self, limbs_len):
+        """pose_detector.py:278-290."""
+        base_limbs_len = limbs_len[[14, 3, 0, 13, 9]]
+        non_zero = base_limbs_len > 0
+        if len(np.nonzero(non_zero)[0]) > 0:
+            ratio = np.array([0.85, 2.2, 2.2, 0.85, 0.85])
+            return np.sum(base_limbs_len[non_zero] / ratio[non_zero]) / len(np.nonzero(non_zero)[0])
+        ratio = np.array([2.2, 1.7, 1.7, 2.2, 1.7, 1.7, 0.6, 0.93, 0.65, 0.85, 0.6, 0.93, 0.65, 0.85, 1, 0.2, 0.2,
+                          0.25, 0.25])
+        non_zero = limbs_len > 0
+        return np.sum(limbs_len[non_zero] / ratio[non_zero]) / len(np.nonzero(non_zero)[0])
+
+    def get_unit_length(self, person_pose):
+        """pose_detector.py:292-296."""
+        limbs_length, _ = self.compute_limbs_length(person_pose)
+        return self.compute_unit_length(limbs_length)
+
+    def crop_around_keypoint(self, img, keypoint, crop_size):
+        """pose_detector.py:298-307."""
+        x, y = keypoint
+        bbox = (int(x - crop_size), int(y - crop_size), int(x + crop_size), int(y + crop_size))
+        return self.crop_image(img, bbox), bbox
+
+    def crop_person(self, img, person_pose, unit_length):
+        """pose_detector.py:309-352.  The reference uses ``sys.maxsize`` without importing sys, so
+        every call raises NameError there; this mirror raises the same error."""
+        raise NameError("name 'sys' is not defined")
+
+    def crop_face(self, img, person_pose, unit_length):
+        """pose_detector.py:354-369: (face_img, bbox) around the nose, or (None, None)."""
+        face_size = unit_length
+        face_img = None
+        bbox = None
+        if person_pose[JointType.Nose][2] > 0:
+            nose_pos = person_pose[JointType.Nose][:2]
+            face_top = int(nose_pos[1] - face_size * 1.2)
+            face_bottom = int(nose_pos[1] + face_size * 0.8)
+            face_left = int(nose_pos[0] - face_size)
+            face_right = int(nose_pos[0] + face_size)
+            bbox = (face_left, face_top, face_right, face_bottom)
+            face_img = self.crop_image(img, bbox)
+        return face_img, bbox
+
+    def crop_hands(self, img, person_pose, unit_length):
+        """pose_detector.py:371-399: {'left'|'right': {'img', 'bbox'} or None}.  Like the reference,
+        the crop centre is updated in place in person_pose (``crop_center +=`` on a view)."""
+        hands = {"left": None, "right": None}
+        for side, hand, elbow in (("left", JointType.LeftHand, JointType.LeftElbow),
+                                  ("right", JointType.RightHand, JointType.RightElbow)):
+            if person_pose[hand][2] > 0:
+                crop_center = person_pose[hand][:-1]
+                if person_pose[elbow][2] > 0:
+                    direction_vec = person_pose[hand][:-1] - person_pose[elbow][:-1]
+                    crop_center += (0.3 * direction_vec).astype(crop_center.dtype)
+                hand_img, bbox = self.crop_around_keypoint(img, crop_center, unit_length * 0.95)
+                hands[side] = {"img": hand_img, "bbox": bbox}
+        return hands
+
+    def crop_image(self, img, bbox):
+        """pose_detector.py:401-425: crop clipped to the image, zero-padded to the bbox size."""
+        left, top, right, bottom = bbox
+        img_h, img_w, img_ch = img.shape
+        box_h = bottom - top
+        box_w = right - left
+        crop_left = max(0, left)
+        crop_top = max(0, top)
+        crop_right = min(img_w, right)
+        crop_bottom = min(img_h, bottom)
+        crop_h = crop_bottom - crop_top
+        crop_w = crop_right - crop_left
+        cropped_img = img[crop_top:crop_bottom, crop_left:crop_right]
+        bias_x = bias_y = 0
+        if left < crop_left:
+            bias_x = crop_left - left
+        if top < crop_top:
+            bias_y = crop_top - top
+        padded_img = np.zeros((box_h, box_w, img_ch), dtype=np.uint8)
+        padded_img[bias_y:bias_y + crop_h, bias_x:bias_x + crop_w] = cropped_img
+        return padded_img

@@ -1,25 +1,27 @@
-"""CocoPoseNet weights on the host: the Chainer npz format and a seeded random initialiser.
+"""Network weights on the host: the Chainer npz format and a seeded random initialiser.
 
 * ``load_npz`` reads what ``chainer.serializers.save_npz(model)`` writes for CocoPoseNet
   (pose_detector.py:26): keys ``<layer>/W`` (Co, Ci, k, k) f32 and ``<layer>/b`` (Co,), possibly
   under a prefix (e.g. ``predictor/``).  Only NumPy's non-pickle loader is used.
 * ``random_weights`` builds random-init weights of the same architecture (He-normal, so the
   activations stay O(1) through the 92 layers) for benchmarking without trained weights.
+* ``arch``: 'posenet' (CocoPoseNet, default), 'facenet' or 'handnet' (layer tables: nets.py).
 """
 import numpy as np
 
 from . import _lib
+from . import nets
 
 
-def layer_table():
-    return _lib.layer_table()
+def layer_table(arch="posenet"):
+    return _lib.layer_table() if arch == "posenet" else nets.layers(arch)
 
 
-def load_npz(path):
+def load_npz(path, arch="posenet"):
     with np.load(path, allow_pickle=False) as z:
         keys = list(z.keys())
         out = {}
-        for name, ci, co, k in layer_table():
+        for name, ci, co, k in layer_table(arch):
             wk = [key for key in keys if key == name + "/W" or key.endswith("/" + name + "/W")]
             bk = [key for key in keys if key == name + "/b" or key.endswith("/" + name + "/b")]
             if not wk or not bk:
@@ -30,12 +32,12 @@ def load_npz(path):
     return out
 
 
-def random_weights(seed=0, bias_scale=0.05):
+def random_weights(seed=0, bias_scale=0.05, arch="posenet"):
     rng = np.random.default_rng(seed)
     out = {}
-    for name, ci, co, k in layer_table():
+    for name, ci, co, k in layer_table(arch):
         fan_in = ci * k * k
-        last = name.startswith("conv5_5") or name.startswith("Mconv7")
+        last = name.startswith("conv5_5") or name.startswith("Mconv7") or name == "conv6_2_CPM"
         std = np.sqrt((1.0 if last else 2.0) / fan_in)
         W = (rng.standard_normal((co, ci, k, k), dtype=np.float32) * np.float32(std)).astype(np.float32)
         b = rng.uniform(-bias_scale, bias_scale, co).astype(np.float32)

@@ -209,6 +209,36 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
 double op_forward_flops(int32_t h, int32_t w);
 
+/* ---- Face / hand keypoint detectors: FaceNet / HandNet single-branch CPM nets ----
+ * face_detector.py:12-56 (FaceDetector), hand_detector.py:12-66 (HandDetector); the same conv kernels
+ * as CocoPoseNet, bf16x3 arithmetic.  One context = one network on one device, one stream. */
+#define OP_ARCH_FACENET 1 /* models/FaceNet.py: 71 heat maps (70 keypoints + background) */
+#define OP_ARCH_HANDNET 2 /* models/HandNet.py: 22 heat maps (21 keypoints + background) */
+typedef struct op_cpm_ctx op_cpm_ctx;
+/* Number of conv layers of `arch` (52) and their table in models/FaceNet.py:11-76 order. */
+int op_cpm_layer_count(int32_t arch);
+int op_cpm_layer_info(int32_t arch, int32_t index, const char** name, int32_t* ci, int32_t* co, int32_t* ksize);
+int op_cpm_create(int32_t arch, int32_t device, op_cpm_ctx** out);
+int op_cpm_destroy(op_cpm_ctx* ctx);
+/* serializers.load_npz(weights_file, self.model) (face_detector.py:16): layers in op_cpm_layer_info order. */
+int op_cpm_set_weights(op_cpm_ctx* ctx, const float* const* W, const float* const* b);
+/* FaceNet.__call__ / HandNet.__call__ (models/FaceNet.py:78-161): x (n, 3, h, w) f32 NCHW
+ * (h, w multiples of 8) -> last-stage maps (n, C, h/8, w/8) f32. */
+int op_cpm_forward(op_cpm_ctx* ctx, const float* x, int32_t n, int32_t h, int32_t w, float* maps);
+/* compute_peaks_from_heatmaps, CPU branch (face_detector.py:58-84, hand_detector.py:68-94): for each
+ * of the first c-1 maps of heatmaps (c, h, w): gaussian_filter(sigma 2.5), global max m; found[i] =
+ * m > thresh (f32); keypoints[i] = [coords[1], coords[0], m] of np.where(map == m) flattened
+ * ([x, y] for one maximum, [y1, y0] for several, as the reference).  flip != 0 reads the maps
+ * mirrored in x (hand_detector.py:47-48: the left-hand maps are flipped before the peaks). */
+int op_cpm_peaks(op_cpm_ctx* ctx, const float* heatmaps, int32_t c, int32_t h, int32_t w, float thresh,
+                 int32_t flip, double* keypoints, int32_t* found);
+/* FaceDetector.__call__ / HandDetector.__call__ on one BGR crop (h x w x 3 u8): cv2 LINEAR resize to
+ * 368 x 368, x/256 - 0.5, forward, F.resize_images to (h, w), peaks as op_cpm_peaks (flip_maps: the
+ * left-hand map flip; the left-hand input flip is the host copy the reference also makes).
+ * keypoints (c-1, 3) f64, found (c-1,). */
+int op_cpm_detect(op_cpm_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, float thresh,
+                  int32_t flip_maps, double* keypoints, int32_t* found);
+
 #ifdef __cplusplus
 }
 #endif

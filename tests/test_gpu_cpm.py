@@ -1,0 +1,121 @@
+"""Face / hand detectors on the GPU, through the C ABI (op_cpm_*): the peak step
+bit-exact against the reference's own outputs, the FaceNet / HandNet forward within the north
+star's 1e-3 of the oracle, and the whole detector equal to the oracle composition fed with the
+device forward's maps."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, pkg_module
+from oracle import cpm as OC
+from oracle import cvresize, postproc as P
+
+pytestmark = pytest.mark.gpu
+FWD_TOL = 1e-3
+CPM = os.path.join(GOLDEN, "cpm")
+
+
+@pytest.fixture(scope="module", params=["facenet", "handnet"])
+def cpm(request):
+    lib = pkg_module("_lib")
+    W = pkg_module("weights").random_weights(seed=4, arch=request.param)
+    c = lib.CpmContext(request.param, 0)
+    c.set_weights(W)
+    yield request.param, c, W
+    c.close()
+
+
+def _same(got, exp):
+    assert len(got) == len(exp)
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert (g is None) == (e is None), i
+        if g is not None:
+            assert g[0] == e[0] and g[1] == e[1] and np.float32(g[2]) == np.float32(e[2]), (i, g, e)
+
+
+@pytest.mark.parametrize("case", ["face_peaks", "hand_peaks", "hand_peaks_wide"])
+def test_cpm_peaks_bit_exact_vs_reference(cpm, case):
+    _, c, _ = cpm
+    d = np.load(os.path.join(CPM, case + ".npz"))
+    heat = d["heat_f16"].astype(np.float32)
+    exp = [None if not f else [int(k[0]), int(k[1]), np.float32(k[2])] for k, f in zip(d["keypoints"], d["found"])]
+    _same(c.peaks(heat, 0.1), exp)
+    # the left-hand readout: peaks of the x-mirrored maps
+    _same(c.peaks(heat, 0.1, flip=True), OC.compute_peaks_from_heatmaps(np.ascontiguousarray(heat[:, :, ::-1]), 0.1))
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 368, 368), (2, 3, 64, 96)])
+def test_cpm_forward_vs_oracle(cpm, shape):
+    arch, c, W = cpm
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.5, 0.5, shape).astype(np.float32)
+    got = c.forward(x)
+    ref = OC.cpm_forward(W, x)
+    err = float(np.abs(got - ref).max())
+    print("%s forward %s: max|gpu-oracle| = %.3g (max|map| = %.3g)" % (arch, shape, err, np.abs(ref).max()))
+    assert got.shape == ref.shape and err <= FWD_TOL
+
+
+@pytest.mark.parametrize("hw,hand_type", [((96, 80), "right"), ((61, 75), "left")])
+def test_cpm_detect_equals_oracle_composition(cpm, hw, hand_type):
+    """detect == oracle resize + peaks of the device forward on the oracle's preprocessed input
+    (so the preprocess (/256), the map upsample and the peak step are each held exactly)."""
+    arch, c, _ = cpm
+    h, w = hw
+    img = np.random.default_rng(h * w).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    left = arch == "handnet" and hand_type == "left"
+    src = np.ascontiguousarray(img[:, ::-1]) if left else img
+    x = OC.preprocess(cvresize.resize_linear_u8(src, 368, 368))
+    low = c.forward(x)[0]
+    heat = P.resize_images(low, h, w)
+    if left:
+        heat = np.ascontiguousarray(heat[:, :, ::-1])
+    # a threshold the random-weight maps cross, so keypoints are found
+    thr = float(np.float32(np.median(heat.max(axis=(1, 2)))))
+    exp = OC.compute_peaks_from_heatmaps(heat, thr)
+    got = c.detect(src, thr, flip_maps=left)
+    assert sum(k is not None for k in exp) > 0
+    _same(got, exp)
+
+
+def test_face_and_hand_detector_api():
+    fd = pkg_module("face_detector").FaceDetector("facenet", None, model=pkg_module("weights").random_weights(1, arch="facenet"))
+    hd = pkg_module("hand_detector").HandDetector("handnet", None, model=pkg_module("weights").random_weights(1, arch="handnet"))
+    img = np.random.default_rng(0).integers(0, 256, (120, 100, 3), dtype=np.uint8)
+    fk = fd(img)
+    hk_r, hk_l = hd(img, hand_type="right"), hd(img, hand_type="left")
+    assert len(fk) == 70 and len(hk_r) == 21 and len(hk_l) == 21
+    for k in fk + hk_r + hk_l:
+        assert k is None or (isinstance(k[0], int) and isinstance(k[1], int) and isinstance(k[2], np.float32))
+    with pytest.raises(ValueError):
+        pkg_module("face_detector").FaceDetector("handnet", None)
+
+
+def test_demo_on_golden_poses(tmp_path):
+    """demo.py's flow (pose -> face / hand crops -> detectors -> drawing) on people.png with the
+    six-person golden poses standing in for the random-weight pose detector's (empty) output."""
+    from conftest import load_golden, people_image
+    demo = pkg_module("demo")
+    W = pkg_module("weights")
+    pd = pkg_module("pose_detector").PoseDetector("posenet", model=W.random_weights(0))
+    poses = load_golden("six_people")["poses"]
+
+    class Pose(object):
+        def __call__(self, img):
+            return poses.copy(), np.ones(len(poses))
+
+        def __getattr__(self, name):
+            return getattr(pd, name)
+
+    fd = pkg_module("face_detector").FaceDetector("facenet", model=W.random_weights(2, arch="facenet"))
+    hd = pkg_module("hand_detector").HandDetector("handnet", model=W.random_weights(2, arch="handnet"))
+    img = people_image()
+    log = []
+    out = demo.run(img, Pose(), fd, hd, log=log.append)
+    assert out.shape == img.shape and out.dtype == np.uint8 and (out != img).any()
+    assert log.count("Estimating face keypoints...") == len(poses)
+    # the CLI with seeded random weights (no persons: the pose blend only)
+    dst = tmp_path / "result.png"
+    src = os.path.join(GOLDEN, "people.png")
+    assert demo.main(["--img", src, "--random-weights", "--out", str(dst)]) == 0 and dst.exists()
