@@ -44,6 +44,26 @@ constexpr int kCatHeat = 128;  // 19 channels (+1 zero pad)
 constexpr int kCatPaf = 152;   // 38 channels (+2 zero pad); 8-channel aligned for the split format
 constexpr int kStagePad = 3;   // halo of the 7x7 stage convs
 
+// ---- LDS DMA: global_load_lds_dwordx4 (lane l's 16 B land at lds + 16 l; lds wave-uniform) ----
+// OP_ASM_DMA=1 issues it from inline asm.  With the builtin anywhere in a kernel the compiler's
+// waitcnt pass makes every later LDS read wait for lgkmcnt(0) (in the 7x7 loop: every second 16-px
+// block waits for the B fragment issued just before); the asm form is invisible to that pass and
+// the reads get exact lgkmcnt(N).  Measured (interleaved A/B, tools/ab_lib.py): no gain -- the
+// second wave of the SIMD already covers those stalls -- so the builtin stays the default.  The
+// asm form writes M0 without telling the compiler; no kernel here relies on M0 otherwise.
+#ifndef OP_ASM_DMA
+#define OP_ASM_DMA 0
+#endif
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
+#if OP_ASM_DMA
+  const uint32_t a =
+      __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "memory");
+#else
+  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+#endif
+}
+
 // ---- launch helpers implemented in the .hip files ----
 struct ConvGroup {
   const float* in;    // padded NHWC input, already offset by the group's first input channel

@@ -246,8 +246,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     if (it >= n_it) it = n_it - 1;           // trailing copies: never read
 #pragma unroll
     for (int i = 0; i < NWP; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + (int64_t)it * wstep), LDS_PTR_G(dst + wdst[i]), 16,
-                                       0, 0);
+      glds16((const void*)(wsrc[i] + (int64_t)it * wstep), dst + wdst[i]);
   };
 
   // this lane's output pixels: tile-local p = (pg*NPB + pb)*32 + l32 -> (r, c) -> halo slot
@@ -301,8 +300,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     const int ppt = (np_w + KSQ - 2) / (KSQ - 1);        // per tap, all issued by tap KSQ-2
     auto halo_piece = [&](const char* src0, char* dst, int hr, int hc) {
       const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
-                                       16, 0, 0);
+      glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
     };
     {  // chunk 0, whole
       int hr = h_r0, hc = h_c0;
@@ -383,8 +381,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
         const bool in_a = hr < rowsA;  // raster tiles: halo rows past rowsA belong to frame fb
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(x0 - R + hc + s.pin, wp_in - 1);
-        __builtin_amdgcn_global_load_lds((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes),
-                                         LDS_PTR_G(dst), 16, 0, 0);
+        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += HSTEP * 1024;
         hc += HSTEP * 64;
         while (hc >= tl.pitch) {
@@ -618,7 +615,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   auto stage_w = [&](int it) {
     char* dst = lds + (it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
-    __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)it * wstep), LDS_PTR_G(dst + wdst), 16, 0, 0);
+    glds16((const void*)(wsrc + (int64_t)it * wstep), dst + wdst);
   };
 
   uint32_t qp[(NPX + 1) / 2];  // this lane's pixel of each block -> halo slot (two per register)
@@ -662,8 +659,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       const int c = p / NPAIR, j = p - (p / NPAIR) * NPAIR;
       const int ia = c * KSQ + 2 * j;
       const int ib = 2 * j + 1 < KSQ ? ia + 1 : ia;
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)ia * wstep), LDS_PTR_G(dst), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)ib * wstep), LDS_PTR_G(dst + SLOT_W), 16, 0, 0);
+      glds16((const void*)(wsrc + (int64_t)ia * wstep), dst);
+      glds16((const void*)(wsrc + (int64_t)ib * wstep), dst + SLOT_W);
     };
     auto tap_off = [&](int j) -> int {
       const int tt = 2 * j + 1 < KSQ ? 2 * j + tsel : 2 * j;
@@ -694,8 +691,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
           const bool in_a = hr < rowsA;
           const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
           const int xx = min(hc - R + s.pin, wp_in - 1);
-          __builtin_amdgcn_global_load_lds(
-              (const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst), 16, 0, 0);
+          glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
           dst += 2 * 1024;
           hc += 2 * 64;
           while (hc >= tl.pitch) {
@@ -768,8 +764,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(hc - R + s.pin, wp_in - 1);
-        __builtin_amdgcn_global_load_lds((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes),
-                                         LDS_PTR_G(dst), 16, 0, 0);
+        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 2 * 1024;
         hc += 2 * 64;
         while (hc >= tl.pitch) {
@@ -944,8 +939,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
       const int cj = j >> 3, pl = (j >> 1) & 3, hf = j & 1;
       const char* src = (const char*)g.w + ((int64_t)(2 * cp + cj) * KSQ + t) * wstep + pl * wplane +
                         ((int64_t)co0 + 64 * hf + lane) * 16;
-      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR_G(dst + cj * CHUNK_W + pl * PLANE_W + hf * 1024), 16,
-                                       0, 0);
+      glds16((const void*)src, dst + cj * CHUNK_W + pl * PLANE_W + hf * 1024);
     }
   };
 
@@ -983,8 +977,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
       int hr = lane / tl.pitch, hc = lane - (lane / tl.pitch) * tl.pitch;
       for (int i = 0; i < tl.nh; ++i) {
         const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), LDS_PTR_G(dst),
-                                         16, 0, 0);
+        glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 1024;
         hc += 64;
         while (hc >= tl.pitch) {
