@@ -23,14 +23,39 @@ METRIC = "frames/sec end-to-end (CNN+PAF grouping) at 368×368, 1/2/4/8 MI355X"
 FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA peak
 HBM_PEAK_GBS = 8000.0
+PARAMS_SCALES = [0.5, 1, 1.5, 2]  # entity.py:74 inference_scales
 
 
-def synthetic_maps(batch):
-    """COCO-like last-stage maps (38 PAF + 19 heat at 46x46) of 6 people, from the reference's own
-    label generators (tests/golden/six_people.npz, made by tests/golden/make_golden.py)."""
-    d = np.load(os.path.join(REPO, "tests", "golden", "six_people.npz"))
+def precise_net(h, w, scale, size=368, stride=8):
+    """detect_precise's padded network input for one scale (pose_detector.py:440-447): (net_h, net_w)."""
+    import math
+    m = scale * size / min(h, w)
+    rh, rw = math.ceil(h * m), math.ceil(w * m)
+    return rh + (-rh) % stride, rw + (-rw) % stride
+
+
+def synthetic_maps(batch, lh=46, lw=46):
+    """COCO-like last-stage maps (38 PAF + 19 heat) from the reference's own label generators
+    (tests/golden/*.npz, made by tests/golden/make_golden.py): 6 people at 46x46 (368x368 frames),
+    20 people at 46x82 (1280x720 frames); None for other map sizes."""
+    name = {(46, 46): "six_people", (46, 82): "twenty_720p"}.get((lh, lw))
+    if name is None:
+        return None
+    d = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"))
     m = np.concatenate([d["paf_low"], d["heat_low"]])[None]
     return np.ascontiguousarray(np.repeat(m, batch, axis=0))
+
+
+def optimal_size(h, w, size=368, stride=8):
+    """compute_optimal_size (pose_detector.py:57-73): (net_w, net_h)."""
+    if w < h:
+        ow = size
+        oh = np.round(size * h / w)
+    else:
+        oh = size
+        ow = np.round(size * w / h)
+    ow, oh = int(ow), int(oh)
+    return ow + (-ow) % stride, oh + (-oh) % stride
 
 
 def cpu_baseline(frames, maps, n_frames):
@@ -104,7 +129,17 @@ def main():
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as one captured hipGraph")
     ap.add_argument("--precision", choices=["bf16x3", "fp32"], default="bf16x3",
                     help="conv arithmetic: 3xBF16-split products (f32 accumulate) or exact f32 MFMA")
+    ap.add_argument("--frame", default="368x368",
+                    help="HxW of the synthetic frames (BASELINE configs: 368x368 = C2/C3, the default "
+                         "and the headline; 720x1280 = C5's 720p stream, single scale)")
+    ap.add_argument("--precise", action="store_true",
+                    help="C4: multi-scale detect_precise (4 scales, cubic resizes) on the staged batch "
+                         "(op_run_staged_precise: one batched forward per scale)")
     args = ap.parse_args()
+    FH, FW = (int(v) for v in args.frame.lower().split("x"))
+    headline = (FH, FW) == (368, 368) and not args.precise
+    if not headline:
+        args.no_cpu_baseline = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,19 +165,30 @@ def main():
     Fr = importlib.import_module(PKG + ".frames")
 
     B = args.batch
+    net_w, net_h = optimal_size(FH, FW)
     halo_mode = int(os.environ.get("OP_HALO_MODE", "4"))
     limits = L.OpLimits()
     limits.max_batch = B
     ctx = L.Context(local, None, limits)
     ctx.set_precision(args.precision)
-    ctx.set_weights(Wm.random_weights(seed=0))
+    wts = Wm.random_weights(seed=0)
+    if args.precise:
+        # the random network's 1280x720 maps are noise with thousands of spurious peaks per joint
+        # (past the per-frame caps); a -1 bias on the last stage's Mconv7 keeps them below the peak
+        # threshold -- same FLOPs, the post-process still runs its full-resolution passes
+        for k in ("Mconv7_stage6_L1", "Mconv7_stage6_L2"):
+            wts[k] = (wts[k][0], wts[k][1] - np.float32(1.0))
+    ctx.set_weights(wts)
     rng = np.random.default_rng(1234 + rank)
-    frames = rng.integers(0, 256, (B, 368, 368, 3), dtype=np.uint8)
+    frames = rng.integers(0, 256, (B, FH, FW, 3), dtype=np.uint8)
+    maps = synthetic_maps(B, net_h // 8, net_w // 8)
+    if maps is None or args.precise:
+        args.maps = "network"
     ctx.stage_frames(frames)
-    maps = synthetic_maps(B)
-    if args.maps == "synthetic":
-        ctx.stage_maps(maps)
-        ctx.use_staged_maps(True)
+    if not args.precise:
+        if args.maps == "synthetic":
+            ctx.stage_maps(maps)
+            ctx.use_staged_maps(True)
 
     def barrier():
         if dist is not None:
@@ -155,9 +201,13 @@ def main():
 
     def step(collect):
         nonlocal persons
-        ctx.run_staged(graph=bool(args.graph))
-        ctx.synchronize()
-        res = ctx.fetch_results(0, B)
+        if args.precise:
+            ctx.run_staged_precise()
+            res = ctx.fetch_results(0, B)
+        else:
+            ctx.run_staged(graph=bool(args.graph))
+            ctx.synchronize()
+            res = ctx.fetch_results(0, B)
         if collect:
             persons += sum(r[2].n_persons for r in res)
         if dist is not None:
@@ -188,8 +238,11 @@ def main():
     ctx.profile_reset()
     n_extra = 0 if args.no_profile else 3
     for _ in range(n_extra):
-        ctx.run_staged()
-        ctx.synchronize()
+        if args.precise:
+            step(False)
+        else:
+            ctx.run_staged()
+            ctx.synchronize()
     prof_all = ctx.profile_read()
     ctx.profile(False)
     if dist is not None:
@@ -222,20 +275,28 @@ def main():
                     "launch_ms": round(ms7 / n7, 4), "flops_per_launch": fl7 / n7,
                     "algorithmic_bytes_per_launch": by7 / n7}
     stage_ms = {k: round(v[0] / n_extra, 3) for k, v in prof_all.items()} if n_extra else {}
+    metric = METRIC if headline else "frames/sec end-to-end (CNN+PAF grouping) at %dx%d%s, 1/2/4/8 MI355X" % (
+        FW, FH, " multi-scale (%s)" % "/".join(str(v) for v in PARAMS_SCALES) if args.precise else "")
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "metric": metric, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16x3 (hi/lo split operands, f32 accumulate)" if args.precision == "bf16x3" else "f32",
-        "data": "synthetic: seeded uint8 368x368 BGR frames resident in HBM; random-init CocoPoseNet (He-normal); "
-                + ("post-process fed COCO-like 6-person network maps (reference label generators)"
-                   if args.maps == "synthetic" else "post-process fed the network's own last stage"),
-        "config": {"workload": "368x368 frames, full PoseDetector.__call__ path (resize+normalise, 92-conv "
-                               "CocoPoseNet fp32, PAF post-process), batch of %d frames per GPU per step" % B,
-                   "frames_per_step_per_gpu": B, "net_input": "368x368", "heatmap": "320x320",
+        "data": "synthetic: seeded uint8 %dx%d BGR frames %s; random-init CocoPoseNet (He-normal); " % (
+            FW, FH, "resident in HBM (last-stage biases -1: no spurious peaks on the random network's "
+                    "full-resolution maps)" if args.precise else "resident in HBM")
+                + ("post-process fed COCO-like %s network maps (reference label generators)"
+                   % ("6-person" if (FH, FW) == (368, 368) else "20-person") if args.maps == "synthetic"
+                   else "post-process fed the network's own last stage"),
+        "config": {"workload": "%dx%d frames, full PoseDetector.%s path (resize+normalise, 92-conv "
+                               "CocoPoseNet fp32, PAF post-process), batch of %d frames per GPU per step"
+                               % (FW, FH, "detect_precise" if args.precise else "__call__", B),
+                   "frames_per_step_per_gpu": B, "net_input": "%dx%d" % (net_w, net_h),
+                   "heatmap": "%dx%d" % optimal_size(FH, FW, 320) if not args.precise else "%dx%d" % (FW, FH),
                    "maps": args.maps, "parallelism": "frame-parallel replicas x%d (RCCL gather of results)" % world},
         "persons_per_s": round(persons / elapsed, 2),
-        "gflop_per_frame": round(L.forward_flops(368, 368) / 1e9, 2),
+        "gflop_per_frame": round((sum(L.forward_flops(*precise_net(FH, FW, sc)) for sc in PARAMS_SCALES)
+                                  if args.precise else L.forward_flops(net_h, net_w)) / 1e9, 2),
         "stage_ms_per_step": stage_ms,
         "stage_ms_note": "HIP-event sums per kernel class over %d untimed profiled steps" % n_extra,
         "roofline": roofline,

@@ -25,7 +25,7 @@ EXPORTED = (
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
-    "op_set_conv_algo", "op_profile_classes",
+    "op_set_conv_algo", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect",
 )
@@ -96,6 +96,7 @@ def lib():
         "op_use_staged_maps": ([P, I32], ctypes.c_int),
         "op_run_staged": ([P], ctypes.c_int),
         "op_run_staged_graph": ([P], ctypes.c_int),
+        "op_run_staged_precise": ([P], ctypes.c_int),
         "op_synchronize": ([P], ctypes.c_int),
         "op_fetch_result": ([P, I32, P, P, I32, P], ctypes.c_int),
         "op_last_timing": ([P, P, P, P], ctypes.c_int),
@@ -376,6 +377,10 @@ class Context(object):
 
     def run_staged(self, graph=False):
         check((lib().op_run_staged_graph if graph else lib().op_run_staged)(self.h), "op_run_staged")
+
+    def run_staged_precise(self):
+        """detect_precise on every staged frame (batched per scale; op_run_staged_precise)."""
+        check(lib().op_run_staged_precise(self.h), "op_run_staged_precise")
 
     def synchronize(self):
         check(lib().op_synchronize(self.h), "op_synchronize")

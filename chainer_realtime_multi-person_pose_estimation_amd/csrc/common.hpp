@@ -163,6 +163,10 @@ int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, 
                             int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);
 int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
                             float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st);
+// planar source (c*cstride + y*sstride + x) -> planar destination, modes 1-3 (precise.hip)
+int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t sstride, int32_t sh, int32_t sw,
+                                   int32_t cn, float* dst, int32_t dh, int32_t dw, int32_t mode, float div,
+                                   hipStream_t st);
 int launch_resize_cubic_u8(const uint8_t* src, int64_t sstride, int32_t sh, int32_t sw, int32_t cn, uint8_t* dst,
                            int32_t dh, int32_t dw, hipStream_t st);
 
@@ -221,10 +225,11 @@ struct MapSource {
 
 int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, hipStream_t st);
 // Sub-steps on already-upsampled inputs (stage-level ABI)
+// full-resolution planar maps; fstride = floats between frames (0: 18 joint planes per frame)
 int launch_peaks_from_full(const float* heat_full, int32_t n_joint, int32_t mh, int32_t mw, const PostShape& s,
-                           PostBuffers& b, hipStream_t st);
+                           PostBuffers& b, hipStream_t st, int64_t fstride = 0);
 int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const PostShape& s, PostBuffers& b,
-                            hipStream_t st);
+                            hipStream_t st, int64_t fstride = 0);
 int launch_grouping(const PostShape& s, PostBuffers& b, hipStream_t st);
 int launch_resize_images(const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y,
                          hipStream_t st);

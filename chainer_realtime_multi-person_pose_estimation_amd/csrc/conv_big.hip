@@ -47,6 +47,7 @@ struct BigTiling {
   int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
   int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
   int32_t hw, total;         // raster tiles: pixels per frame, pixels of the batch
+  int32_t fa_tiles;          // > 0 (conv_m16): raster tiles aligned to frames, fa_tiles per frame
   int32_t per_xcd;           // > 0: pixel-major XCD order (conv_m16k): XCD x runs pixel tiles
                              // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
 };
@@ -586,8 +587,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int co0 = (unit - grp * tl.co_tiles) * CW;
   const SplitConvGroup g = grp == 0 ? g0 : g1;
   if (co0 >= g.cop) return;
-  const int P0 = widx * CAP;
-  const int P1 = min(P0 + CAP, tl.total) - 1;
+  int P0, P1;
+  if (tl.fa_tiles) {  // frame-aligned raster tiles (wide maps): one frame per tile, last one partial
+    const int f = widx / tl.fa_tiles;
+    P0 = f * tl.hw + (widx - f * tl.fa_tiles) * CAP;
+    P1 = min(P0 + CAP, (f + 1) * tl.hw) - 1;
+  } else {
+    P0 = widx * CAP;
+    P1 = min(P0 + CAP, tl.total) - 1;
+  }
   const int frame = P0 / tl.hw;
   const int y0 = (P0 - frame * tl.hw) / s.w;
   const int fb = P1 / tl.hw;
@@ -1208,21 +1216,37 @@ static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const 
 // (46 x 46 maps: 2116 px = 2.76 tiles of 768, where rectangular tiles pay 3).  The halo holds the
 // tile's rows of each frame with their own KS-1 border rows; every frame is >= cap pixels, so a
 // tile touches at most two.  false when the worst tile's halo does not fit LDS.
-static bool raster_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t) {
+// wide: (conv_m16 only) when the batch-raster halo does not fit, also try the tight pitch (blocks
+// that wrap a row then see a few 2-way bank conflicts) and then frame-aligned raster tiles (no
+// tile crosses a frame: one border region instead of two; the last tile of a frame is partial),
+// so the wide maps of the multi-scale path (82 .. 164 columns) stay on the raster kernel.
+static bool raster_tiling(const BigConfig& k, int n, int h, int w, int groups, int cop_max, BigTiling& t,
+                          bool wide = false) {
   const int cap = k.cap(), hw = h * w, R = k.ks / 2;
   const int64_t total = (int64_t)n * hw;
   if (hw < cap || total >= (1 << 30)) return false;
-  const int tiles = (int)((total + cap - 1) / cap);
-  int rows_max = 0;
-  for (int i = 0; i < tiles; ++i) {
-    const int P0 = i * cap, P1 = (int)std::min<int64_t>((int64_t)P0 + cap, total) - 1;
-    const int fa = P0 / hw, ya = (P0 - fa * hw) / w, fb = P1 / hw, yb = (P1 - fb * hw) / w;
-    const int rows = fa == fb ? yb - ya + 1 + 2 * R : (h - ya + 2 * R) + (yb + 1 + 2 * R);
-    rows_max = std::max(rows_max, rows);
+  const int budget = k.lds_budget() - k.ring_bytes();
+  int tiles = 0, rows_max = 0, pitch = 0, nh = 0, fa = 0;
+  bool ok = false;
+  for (int variant = 0; variant < (wide ? 4 : 1) && !ok; ++variant) {
+    const bool aligned = variant >= 2;
+    pitch = (variant & 1) ? w + k.ks - 1 : halo_pitch(w, k.ks);
+    fa = aligned ? (hw + cap - 1) / cap : 0;
+    tiles = aligned ? n * fa : (int)((total + cap - 1) / cap);
+    rows_max = 0;
+    const int nt = aligned ? fa : tiles;  // aligned: every frame has the same tiles
+    for (int i = 0; i < nt; ++i) {
+      const int P0 = i * cap;
+      const int P1 = (int)std::min<int64_t>((int64_t)P0 + cap, aligned ? hw : total) - 1;
+      const int f0 = P0 / hw, ya = (P0 - f0 * hw) / w, f1 = P1 / hw, yb = (P1 - f1 * hw) / w;
+      const int rows = f0 == f1 ? yb - ya + 1 + 2 * R : (h - ya + 2 * R) + (yb + 1 + 2 * R);
+      rows_max = std::max(rows_max, rows);
+    }
+    nh = (rows_max * pitch + 63) / 64;
+    ok = 4 * nh * 1024 <= budget && nh * 64 < 65536;
   }
-  const int pitch = halo_pitch(w, k.ks);
-  const int nh = (rows_max * pitch + 63) / 64;
-  if (4 * nh * 1024 > k.lds_budget() - k.ring_bytes() || nh * 64 >= 65536) return false;
+  if (!ok) return false;
+  t.fa_tiles = fa;
   t.tr = 0;
   t.tc = w;
   t.tiles_y = tiles;
@@ -1380,7 +1404,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   if (s.ks == 7) {
     if (!c128) return OP_OK;
     if (s.halo_mode != 9 && s.halo_mode != 10 && s.halo_mode != 11 &&
-        raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
+        raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
       if (plain_order) tl.xpu = 0;
       *taken = 1;

@@ -74,13 +74,15 @@ __device__ __forceinline__ int cv_cubic_u8(const uint8_t* src, int64_t sstride, 
   return clampc(r, 0, 255);
 }
 
-// One f32 output element; src element (y, x, ch) at src[y*sstride + x*pstride + ch].
+// One f32 output element; src element (y, x, ch) at src[y*sstride + x*pstride + ch*cstride]
+// (interleaved: cstride 1; planar: pstride 1, cstride = plane size).
 __device__ __forceinline__ float cv_cubic_f32(const float* src, int64_t sstride, int pstride, int sh, int sw, int ch,
-                                              const CubicTap& tx, const CubicTap& ty, int e, int simd_end) {
+                                              const CubicTap& tx, const CubicTap& ty, int e, int simd_end,
+                                              int64_t cstride = 1) {
   float hs[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float* row = src + (int64_t)clampc(ty.s - 1 + k, 0, sh - 1) * sstride + ch;
+    const float* row = src + (int64_t)clampc(ty.s - 1 + k, 0, sh - 1) * sstride + ch * cstride;
     float v = __fmul_rn(row[(int64_t)clampc(tx.s - 1, 0, sw - 1) * pstride], tx.c[0]);
     v = __fadd_rn(v, __fmul_rn(row[(int64_t)clampc(tx.s, 0, sw - 1) * pstride], tx.c[1]));
     v = __fadd_rn(v, __fmul_rn(row[(int64_t)clampc(tx.s + 1, 0, sw - 1) * pstride], tx.c[2]));

@@ -120,7 +120,7 @@ struct PafLow {
     return up_sample(m, off + c, up_tap(y, x, lh, lw, mh, mw));
   }
 };
-struct PafFull {
+struct PafFull {  // planar (38, mh, mw) of one frame (limb_pairs_full offsets p per frame)
   const float* p;
   int mh, mw;
   __device__ __forceinline__ float at(int c, int y, int x) const { return p[((int64_t)c * mh + y) * mw + x]; }
@@ -201,9 +201,10 @@ __global__ __launch_bounds__(256) void limb_pairs_low(MapSource src, PostShape s
   limb_pairs_body(paf, s, b, f, l);
 }
 
-__global__ __launch_bounds__(256) void limb_pairs_full(const float* __restrict__ paf_full, PostShape s, PostBuffers b) {
+__global__ __launch_bounds__(256) void limb_pairs_full(const float* __restrict__ paf_full, int64_t fstride, PostShape s,
+                                                       PostBuffers b) {
   PafFull paf;
-  paf.p = paf_full;
+  paf.p = paf_full + blockIdx.x * fstride;
   paf.mh = s.mh;
   paf.mw = s.mw;
   limb_pairs_body(paf, s, b, blockIdx.x, blockIdx.y);
@@ -478,12 +479,13 @@ struct HeatLow {  // heat channels of the low-res stage output, upsampled on the
   MapSource src;
   int lh, lw, mh, mw;
 };
-struct HeatFull {  // already-upsampled planes [f*18 + j][mh][mw]
+struct HeatFull {  // already-upsampled planes: frame f, joint j at p + f*fs + j*mh*mw
   static constexpr bool kLow = false;
   const float* p;
   int mh, mw;
+  int64_t fs;
   __device__ __forceinline__ float at(int f, int j, int y, int x) const {
-    return p[(((int64_t)f * OP_N_JOINTS + j) * mh + y) * mw + x];
+    return p[f * fs + ((int64_t)j * mh + y) * mw + x];
   }
 };
 
@@ -764,7 +766,7 @@ int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, h
 }
 
 int launch_peaks_from_full(const float* heat_full, int32_t n_joint, int32_t mh, int32_t mw, const PostShape& s,
-                           PostBuffers& b, hipStream_t st) {
+                           PostBuffers& b, hipStream_t st, int64_t fstride) {
   (void)n_joint;
   (void)mh;
   (void)mw;
@@ -774,17 +776,18 @@ int launch_peaks_from_full(const float* heat_full, int32_t n_joint, int32_t mh, 
   hs.p = heat_full;
   hs.mh = s.mh;
   hs.mw = s.mw;
+  hs.fs = fstride ? fstride : (int64_t)OP_N_JOINTS * s.mh * s.mw;
   return run_heat_tiled(hs, s, b, st);
 }
 
 int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const PostShape& s, PostBuffers& b,
-                            hipStream_t st) {
+                            hipStream_t st, int64_t fstride) {
   (void)mh;
   (void)mw;
   int rc = check_shape(s, b);
   if (rc) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
-  hipLaunchKernelGGL(limb_pairs_full, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, paf_full, s, b);
+  hipLaunchKernelGGL(limb_pairs_full, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, paf_full, fstride, s, b);
   OP_AFTER_LAUNCH("limb_pairs_full", st);
   hipLaunchKernelGGL(limb_greedy, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
   OP_AFTER_LAUNCH("limb_greedy", st);

@@ -116,6 +116,45 @@ int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, 
   return OP_OK;
 }
 
+// The same resize from a PLANAR source (element (y, x, c) at src[c*cstride + y*sstride + x]) into a
+// planar destination (modes 1-3 as above); block = 256 consecutive x of one (row, channel), so the
+// row's taps are block-uniform and the source rows are read coalesced.  Values identical to
+// resize_cubic_f32 on the interleaved copy of the source (OpenCV's SIMD/tail split still follows
+// the interleaved element index x*cn + c).
+__global__ __launch_bounds__(256) void resize_cubic_f32_planar(const float* __restrict__ src, int64_t cstride,
+                                                               int64_t sstride, int sh, int sw, int cn,
+                                                               float* __restrict__ dst, int dh, int dw, int mode,
+                                                               float div) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y, c = blockIdx.z;
+  if (x >= dw) return;
+  const CubicTap tx = cv_cubic_tap(x, dw, sw);
+  const CubicTap ty = cv_cubic_tap(y, dh, sh);
+  const float v = cv_cubic_f32(src, sstride, 1, sh, sw, c, tx, ty, x * cn + c, dw * cn / 4 * 4, cstride);
+  const int64_t i = ((int64_t)c * dh + y) * dw + x;
+  if (mode == 1) {
+    dst[i] = v;
+  } else if (mode == 2) {
+    dst[i] = __fadd_rn(dst[i], v);
+  } else {
+    dst[i] = __fdiv_rn(__fadd_rn(dst[i], v), div);
+  }
+}
+
+int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t sstride, int32_t sh, int32_t sw,
+                                   int32_t cn, float* dst, int32_t dh, int32_t dw, int32_t mode, float div,
+                                   hipStream_t st) {
+  if (mode < 1 || mode > 3) {
+    set_error("resize_cubic_f32_planar: planar modes are 1..3");
+    return OP_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(resize_cubic_f32_planar, dim3((unsigned)((dw + 255) / 256), (unsigned)dh, (unsigned)cn),
+                     dim3(256), 0, st, src, cstride, sstride, sh, sw, cn, dst, dh, dw, mode, div);
+  OP_AFTER_LAUNCH("resize_cubic_f32_planar", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 // Generic cv2.resize(INTER_CUBIC) of a cn-channel uint8 image (row stride sstride bytes) to a
 // contiguous dh x dw x cn image (the stage-level ABI op_resize_cubic).
 __global__ __launch_bounds__(256) void resize_cubic_u8(const uint8_t* __restrict__ src, int64_t sstride, int sh, int sw,

@@ -235,9 +235,19 @@ struct op_ctx {
   PackedConv st_g[5][2][5];    // [stage][branch][Mconv2..Mconv6]
   PackedConv st_last[5][2];    // Mconv7
   float* w11 = nullptr;        // conv1_1 weights [tap][ci][co] f32 for the VALU kernel (conv11.hip)
-  // activation arena
+  // activation arena of the current geometry, and every geometry's arena (multi-scale: one per
+  // scale, kept so switching scales needs neither an allocation nor a re-zeroing memset)
   void* arena = nullptr;
   size_t arena_bytes = 0;
+  struct GeomArena {
+    int n, h, w;
+    bool split;
+    void* p;
+    size_t bytes;
+    uint64_t used;
+  };
+  std::vector<GeomArena> arenas;
+  uint64_t arena_clock = 0;
   int gn = 0, gh = 0, gw = 0;  // current geometry (batch, net h, net w)
   bool split = true;           // 3xBF16 split convs (default) or exact f32 MFMA convs
   bool gsplit = true;          // format the arena is currently carved for
@@ -254,6 +264,8 @@ struct op_ctx {
   uint8_t* d_frames = nullptr;
   size_t frames_bytes = 0;
   int st_n = 0, st_h = 0, st_w = 0;
+  bool st_precise = false;     // the staged results come from op_run_staged_precise
+  int st_net_w = 0, st_net_h = 0;
   float* d_maps = nullptr;
   size_t maps_bytes = 0;
   int sm_n = 0, sm_h = 0, sm_w = 0;
@@ -325,19 +337,35 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   if (c->gn == n && c->gh == h && c->gw == w && c->gsplit == c->split) return OP_OK;
   Act a[B_COUNT];
   const size_t need = geom_floats(c, n, h, w, a, c->split) * sizeof(float);
-  if (need > c->arena_bytes) {
-    if (c->arena) {
+  op_ctx::GeomArena* ga = nullptr;
+  for (auto& e : c->arenas)
+    if (e.n == n && e.h == h && e.w == w && e.split == c->split) ga = &e;
+  if (!ga) {
+    // bounded cache: at most 6 geometries / 96 GiB of arenas, least recently used evicted first
+    const size_t cap_bytes = (size_t)96 << 30;
+    for (;;) {
+      size_t tot = need;
+      for (auto& e : c->arenas) tot += e.bytes;
+      if (c->arenas.empty() || (c->arenas.size() < 6 && tot <= cap_bytes)) break;
+      size_t lru = 0;
+      for (size_t i = 1; i < c->arenas.size(); ++i)
+        if (c->arenas[i].used < c->arenas[lru].used) lru = i;
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-      guard_forget(c->arena, c->arena_bytes);
-      OP_HIP_CHECK(hipFree(c->arena));
+      guard_forget(c->arenas[lru].p, c->arenas[lru].bytes);
+      OP_HIP_CHECK(hipFree(c->arenas[lru].p));
+      c->arenas.erase(c->arenas.begin() + lru);
     }
-    c->arena = nullptr;
-    OP_HIP_CHECK(hipMalloc(&c->arena, need));
-    c->arena_bytes = need;
+    void* p = nullptr;
+    OP_HIP_CHECK(hipMalloc(&p, need));
+    // zero halos (and everything else) once per geometry; kernels only ever write interiors
+    OP_HIP_CHECK(hipMemsetAsync(p, 0, need, c->stream));
+    c->arenas.push_back(op_ctx::GeomArena{n, h, w, c->split, p, need, 0});
+    ga = &c->arenas.back();
   }
-  guard_forget(c->arena, c->arena_bytes);
-  // zero halos (and everything else) once per geometry; kernels only ever write interiors
-  OP_HIP_CHECK(hipMemsetAsync(c->arena, 0, need, c->stream));
+  ga->used = ++c->arena_clock;
+  if (c->arena) guard_forget(c->arena, c->arena_bytes);
+  c->arena = ga->p;
+  c->arena_bytes = ga->bytes;
   float* p = (float*)c->arena;
   for (int i = 0; i < B_COUNT; ++i) {
     a[i].p = p;
@@ -981,12 +1009,16 @@ int op_destroy(op_ctx* c) {
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
   free_weights(c);
-  guard_forget(c->arena, c->arena_bytes);
+  for (auto& e : c->arenas) {
+    guard_forget(e.p, e.bytes);
+    hipFree(e.p);
+  }
+  c->arenas.clear();
+  c->arena = nullptr;
   guard_forget(c->post_arena, c->post_bytes);
   guard_forget(c->d_frames, c->frames_bytes + g_guard);
   guard_forget(c->d_maps, c->maps_bytes + g_guard);
   guard_forget(c->d_scratch, c->scratch_bytes + g_guard);
-  if (c->arena) hipFree(c->arena);
   if (c->post_arena) hipFree(c->post_arena);
   if (c->d_frames) hipFree(c->d_frames);
   if (c->d_maps) hipFree(c->d_maps);
@@ -1387,6 +1419,7 @@ int op_postprocess(op_ctx* c, const float* paf_low, const float* heat_low, int32
 
 // Enqueue preprocess + forward + post-process for the staged batch on the context stream.
 static int enqueue_staged(op_ctx* c, bool timing) {
+  c->st_precise = false;
   using namespace op;
   int in_w, in_h, map_w, map_h;
   optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
@@ -1553,6 +1586,19 @@ int op_synchronize(op_ctx* c) {
   return OP_OK;
 }
 
+// network input / post-process map size of the staged results (single scale or precise)
+static void staged_sizes(op_ctx* c, int* in_w, int* in_h, int* map_w, int* map_h) {
+  if (c->st_precise) {
+    *in_w = c->st_net_w;
+    *in_h = c->st_net_h;
+    *map_w = c->st_w;
+    *map_h = c->st_h;
+    return;
+  }
+  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, in_w, in_h);
+  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, map_w, map_h);
+}
+
 int op_fetch_result(op_ctx* c, int32_t frame, double* poses, double* scores, int32_t cap, op_frame_result* res) {
   using namespace op;
   RC(check_ctx(c, false));
@@ -1562,8 +1608,7 @@ int op_fetch_result(op_ctx* c, int32_t frame, double* poses, double* scores, int
   }
   memset(res, 0, sizeof(*res));
   int in_w, in_h, map_w, map_h;
-  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
-  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  staged_sizes(c, &in_w, &in_h, &map_w, &map_h);
   res->map_w = map_w;
   res->map_h = map_h;
   res->net_w = in_w;
@@ -1582,8 +1627,7 @@ int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double*
   std::vector<int32_t> hdr((size_t)n * 4);
   OP_HIP_CHECK(hipMemcpy(hdr.data(), c->pb.res_hdr + 4 * first, hdr.size() * 4, hipMemcpyDeviceToHost));
   int in_w, in_h, map_w, map_h;
-  optimal_size(c->st_h, c->st_w, c->prm.inference_img_size, 8, &in_w, &in_h);
-  optimal_size(c->st_h, c->st_w, c->prm.heatmap_size, 8, &map_w, &map_h);
+  staged_sizes(c, &in_w, &in_h, &map_w, &map_h);
   int maxp = 0;
   for (int i = 0; i < n; ++i) {
     op_frame_result& r = res[i];
@@ -1654,6 +1698,92 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
 
 // detect_precise (pose_detector.py:433-482).  Sizes follow the reference's Python arithmetic:
 // multiplier = scale * inference_img_size / min(h, w) and math.ceil(w * multiplier) in f64.
+// detect_precise (pose_detector.py:433-482) for the n frames (h x w, contiguous) at c->d_frames:
+// per scale one batched forward of the n frames (cubic resize + pad + normalise per frame), then
+// per frame the cubic map resizes into its running mean (psum: [frame][38 paf | 19 heat][h][w]),
+// then the full-resolution post-process of all n frames (results at frame index f).
+static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h) {
+  const int ds = c->prm.downscale;
+  const int ns = c->prm.n_scales;
+  int rws[OP_MAX_SCALES], rhs[OP_MAX_SCALES], pws[OP_MAX_SCALES], phs[OP_MAX_SCALES];
+  size_t mid_max = 0;
+  for (int k = 0; k < ns; ++k) {
+    const double m = c->prm.inference_scales[k] * (double)c->prm.inference_img_size / (double)(h < w ? h : w);
+    rws[k] = (int)std::ceil((double)w * m);
+    rhs[k] = (int)std::ceil((double)h * m);
+    pws[k] = rws[k] + (ds - rws[k] % ds) % ds;
+    phs[k] = rhs[k] + (ds - rhs[k] % ds) % ds;
+    if (rws[k] < 1 || rhs[k] < 1 || phs[k] < 16 || pws[k] < 16) {
+      set_error("detect_precise: a scale gives a network input below 16 x 16");
+      return OP_ERR_INVALID;
+    }
+    mid_max = std::max(mid_max, (size_t)phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT) * 4);
+  }
+  const int64_t fplanes = (int64_t)(OP_N_PAF + OP_N_HEAT) * h * w;  // floats per frame of psum
+  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_max, "precise_mid"));
+  RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
+  const size_t fbytes = (size_t)h * w * 3;
+  for (int k = 0; k < ns; ++k) {
+    const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
+    RC(ensure_geometry(c, n, ph, pw));
+    const Act& x0 = c->buf[B_X0];
+    for (int f = 0; f < n; ++f)
+      RC(launch_preprocess_cubic(c->d_frames + f * fbytes, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split,
+                                 x0.p + (size_t)f * x0.frame_floats(), c->stream));
+    RC(run_forward(c));
+    // last-stage maps (lh, lw, cs) with the PAF / heat channels at paf_off / heat_off
+    const int lh = ph / 8, lw = pw / 8;
+    const float* mbase;
+    int64_t mrow, mframe;
+    int mpx, paf_off, heat_off;
+    if (c->split) {
+      const Act& m = c->buf[B_MAP32];
+      mbase = m.p;
+      mrow = (int64_t)lw * m.cs;
+      mframe = (int64_t)m.frame_floats();
+      mpx = m.cs;
+      paf_off = 0;
+      heat_off = 40;
+    } else {
+      const Act& cat = c->buf[B_CAT];
+      mrow = (int64_t)(lw + 2 * cat.pad) * cat.cs;
+      mframe = (int64_t)cat.frame_floats();
+      mbase = cat.p + cat.pad * mrow + (int64_t)cat.pad * cat.cs;
+      mpx = cat.cs;
+      paf_off = kCatPaf;
+      heat_off = kCatHeat;
+    }
+    const int mode = k == 0 ? 1 : (k == ns - 1 ? 3 : 2);
+    for (int f = 0; f < n; ++f) {
+      const float* mf = mbase + f * mframe;
+      float* sum_paf = c->d_psum + f * fplanes;
+      float* sum_heat = sum_paf + (size_t)OP_N_PAF * h * w;
+      // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping),
+      // stored planar (cn, ph, pw) so the second resize reads coalesced rows
+      float* mid_paf = c->d_pmid;
+      float* mid_heat = c->d_pmid + (size_t)ph * pw * OP_N_PAF;
+      const int64_t pp = (int64_t)ph * pw;
+      RC(launch_resize_cubic_f32(mf + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 1, 1.0f, c->stream));
+      RC(launch_resize_cubic_f32(mf + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 1, 1.0f, c->stream));
+      // :462-463 / :466-467 crop to rh x rw, cubic to h x w, running sum (mean after the last scale)
+      RC(launch_resize_cubic_f32_planar(mid_paf, pp, pw, rh, rw, OP_N_PAF, sum_paf, h, w, mode, (float)ns, c->stream));
+      RC(launch_resize_cubic_f32_planar(mid_heat, pp, pw, rh, rw, OP_N_HEAT, sum_heat, h, w, mode, (float)ns,
+                                        c->stream));
+    }
+  }
+  // :474-482 post-process at the original resolution: img_len = orig_w, no rescale
+  RC(ensure_post(c, n, h, w));
+  PostShape s;
+  post_shape(c, s, n, h, w, h, w, (double)w, 1.0, 1.0);
+  const float* sum_heat0 = c->d_psum + (size_t)OP_N_PAF * h * w;
+  RC(launch_peaks_from_full(sum_heat0, OP_N_JOINTS, h, w, s, c->pb, c->stream, fplanes));
+  RC(launch_connections_full(c->d_psum, h, w, s, c->pb, c->stream, fplanes));
+  RC(launch_grouping(s, c->pb, c->stream));
+  *net_w = pws[ns - 1];
+  *net_h = phs[ns - 1];
+  return OP_OK;
+}
+
 int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, double* poses,
                       double* scores, int32_t cap, op_frame_result* res, float* pafs_out, float* heat_out) {
   using namespace op;
@@ -1667,72 +1797,10 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
                                 hipMemcpyHostToDevice, c->stream));
   c->st_n = 0;  // the staged frame set is replaced
-  const int ds = c->prm.downscale;
-  const int ns = c->prm.n_scales;
-  // per-scale sizes and the largest intermediate
-  int rws[OP_MAX_SCALES], rhs[OP_MAX_SCALES], pws[OP_MAX_SCALES], phs[OP_MAX_SCALES];
-  size_t mid_max = 0;
-  for (int k = 0; k < ns; ++k) {
-    const double m = c->prm.inference_scales[k] * (double)c->prm.inference_img_size / (double)(h < w ? h : w);
-    rws[k] = (int)std::ceil((double)w * m);
-    rhs[k] = (int)std::ceil((double)h * m);
-    pws[k] = rws[k] + (ds - rws[k] % ds) % ds;
-    phs[k] = rhs[k] + (ds - rhs[k] % ds) % ds;
-    if (rws[k] < 1 || rhs[k] < 1 || phs[k] < 16 || pws[k] < 16) {
-      set_error("op_detect_precise: a scale gives a network input below 16 x 16");
-      return OP_ERR_INVALID;
-    }
-    mid_max = std::max(mid_max, (size_t)phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT) * 4);
-  }
-  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_max, "precise_mid"));
-  RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)h * w * (OP_N_PAF + OP_N_HEAT) * 4, "precise_sum"));
-  float* sum_paf = c->d_psum;
-  float* sum_heat = c->d_psum + (size_t)OP_N_PAF * h * w;
-  for (int k = 0; k < ns; ++k) {
-    const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
-    RC(ensure_geometry(c, 1, ph, pw));
-    RC(launch_preprocess_cubic(c->d_frames, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split, c->buf[B_X0].p,
-                               c->stream));
-    RC(run_forward(c));
-    // last-stage maps (lh, lw, cs) with the PAF / heat channels at paf_off / heat_off
-    const int lh = ph / 8, lw = pw / 8;
-    const float* mbase;
-    int64_t mrow;
-    int mpx, paf_off, heat_off;
-    if (c->split) {
-      const Act& m = c->buf[B_MAP32];
-      mbase = m.p;
-      mrow = (int64_t)lw * m.cs;
-      mpx = m.cs;
-      paf_off = 0;
-      heat_off = 40;
-    } else {
-      const Act& cat = c->buf[B_CAT];
-      mrow = (int64_t)(lw + 2 * cat.pad) * cat.cs;
-      mbase = cat.p + cat.pad * mrow + (int64_t)cat.pad * cat.cs;
-      mpx = cat.cs;
-      paf_off = kCatPaf;
-      heat_off = kCatHeat;
-    }
-    // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping)
-    float* mid_paf = c->d_pmid;
-    float* mid_heat = c->d_pmid + (size_t)ph * pw * OP_N_PAF;
-    RC(launch_resize_cubic_f32(mbase + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 0, 1.0f, c->stream));
-    RC(launch_resize_cubic_f32(mbase + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 0, 1.0f, c->stream));
-    // :462-463 / :466-467 crop to rh x rw, cubic to h x w, running sum (mean after the last scale)
-    const int mode = k == 0 ? 1 : (k == ns - 1 ? 3 : 2);
-    RC(launch_resize_cubic_f32(mid_paf, (int64_t)pw * OP_N_PAF, OP_N_PAF, rh, rw, OP_N_PAF, sum_paf, h, w, mode,
-                               (float)ns, c->stream));
-    RC(launch_resize_cubic_f32(mid_heat, (int64_t)pw * OP_N_HEAT, OP_N_HEAT, rh, rw, OP_N_HEAT, sum_heat, h, w, mode,
-                               (float)ns, c->stream));
-  }
-  // :474-482 post-process at the original resolution: img_len = orig_w, no rescale
-  RC(ensure_post(c, 1, h, w));
-  PostShape s;
-  post_shape(c, s, 1, h, w, h, w, (double)w, 1.0, 1.0);
-  RC(launch_peaks_from_full(sum_heat, OP_N_JOINTS, h, w, s, c->pb, c->stream));
-  RC(launch_connections_full(sum_paf, h, w, s, c->pb, c->stream));
-  RC(launch_grouping(s, c->pb, c->stream));
+  int net_w = 0, net_h = 0;
+  RC(precise_run(c, 1, h, w, &net_w, &net_h));
+  const float* sum_paf = c->d_psum;
+  const float* sum_heat = c->d_psum + (size_t)OP_N_PAF * h * w;
   if (pafs_out)
     OP_HIP_CHECK(hipMemcpyAsync(pafs_out, sum_paf, (size_t)OP_N_PAF * h * w * 4, hipMemcpyDeviceToHost, c->stream));
   if (heat_out)
@@ -1742,9 +1810,24 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   memset(res, 0, sizeof(*res));
   res->map_w = w;
   res->map_h = h;
-  res->net_w = pws[ns - 1];
-  res->net_h = phs[ns - 1];
+  res->net_w = net_w;
+  res->net_h = net_h;
   return read_result(c, 0, poses, scores, cap, res);
+}
+
+int op_run_staged_precise(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (c->st_n < 1 || c->st_h < 11 || c->st_w < 11 || c->prm.n_scales < 1) {
+    set_error("op_run_staged_precise: no staged frames (>= 11 x 11) or no inference scale");
+    return OP_ERR_STATE;
+  }
+  int net_w = 0, net_h = 0;
+  RC(precise_run(c, c->st_n, c->st_h, c->st_w, &net_w, &net_h));
+  c->st_precise = true;
+  c->st_net_w = net_w;
+  c->st_net_h = net_h;
+  return OP_OK;
 }
 
 int op_resize_cubic(op_ctx* c, const void* src, int32_t dtype, int32_t h, int32_t w, int32_t cn, void* dst,

@@ -180,6 +180,11 @@ int op_stage_maps(op_ctx* ctx, const float* maps, int32_t n, int32_t mh, int32_t
 int op_use_staged_maps(op_ctx* ctx, int32_t enable);
 /* Enqueue the full path (resize+normalise, 92 convs, post-process) on the staged frames; async. */
 int op_run_staged(op_ctx* ctx);
+/* detect_precise (pose_detector.py:433-482) on every staged frame: per inference scale one batched
+ * forward of all staged frames, per-frame cubic map resizes into the running mean, then the
+ * full-resolution post-process; results via op_fetch_result(s) as for op_run_staged (map_w/h = the
+ * frame size, net_w/h = the largest scale's network input).  Synchronous on the context stream. */
+int op_run_staged_precise(op_ctx* ctx);
 /* Capture op_run_staged as a hipGraph and replay it (same semantics, fewer launches). */
 int op_run_staged_graph(op_ctx* ctx);
 int op_synchronize(op_ctx* ctx);

@@ -125,6 +125,15 @@ def test_forward_368_vs_oracle(precision_ctx, rand_weights):
     _fwd_check(precision_ctx, rand_weights, x)
 
 
+@pytest.mark.parametrize("shape", [(1, 3, 368, 656), (2, 3, 552, 984), (1, 3, 736, 1312)])
+def test_forward_wide_vs_oracle(ctx, rand_weights, shape):
+    """The multi-scale path's wide maps (82 / 123 / 164 columns): the 7x7 raster kernel with the
+    tight halo pitch and with frame-aligned tiles (conv_big.hip raster_tiling(wide))."""
+    rng = np.random.default_rng(shape[2])
+    x = rng.uniform(-0.5, 0.5, shape).astype(np.float32)
+    _fwd_check(ctx, rand_weights, x)
+
+
 @pytest.mark.parametrize("algo", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_conv_algos_agree(ctx, algo):
     """Every bf16x3 kernel family computes the same forward (batch 2 at 368x368 and 720p-shaped
@@ -254,6 +263,40 @@ def test_detect_precise_vs_oracle(lib, rand_weights_small, prec):
             wp, ws = PR.postprocess_full(pafs, heat, img.shape[1], params)
             assert res.n_peaks == len(P.compute_peaks_from_heatmaps(heat, params))
             assert np.array_equal(poses.reshape(wp.shape), wp) and np.array_equal(scores, ws)
+    finally:
+        c.close()
+
+
+def test_staged_precise_batch_equals_per_frame(lib, rand_weights):
+    """op_run_staged_precise (all staged frames batched per scale) == op_detect_precise per frame:
+    poses, scores and status identical, incl. frames whose noise maps exceed a cap / raise."""
+    W = {k: (w, b.copy()) for k, (w, b) in rand_weights.items()}
+    for k in ("Mconv7_stage6_L1", "Mconv7_stage6_L2"):  # fewer noise peaks on the random maps
+        W[k] = (W[k][0], W[k][1] - np.float32(0.3))
+    limits = lib.OpLimits()
+    limits.max_batch = 3
+    c = lib.Context(0, None, limits)
+    try:
+        c.set_weights(W)
+        frames = np.random.default_rng(9).integers(0, 256, (3, 72, 104, 3), dtype=np.uint8)
+        single = []
+        for f in frames:
+            try:
+                single.append((0,) + tuple(c.detect_precise(f)[:2]))
+            except (IndexError, RuntimeError) as e:
+                single.append((type(e).__name__,))
+        c.stage_frames(frames)
+        c.run_staged_precise()
+        for i in range(3):
+            try:
+                p, s_, r = c.fetch_result(i)
+                got = (0, p, s_)
+                assert r.map_w == 104 and r.map_h == 72
+            except (IndexError, RuntimeError) as e:
+                got = (type(e).__name__,)
+            assert got[0] == single[i][0]
+            if got[0] == 0:
+                assert np.array_equal(got[1], single[i][1]) and np.array_equal(got[2], single[i][2])
     finally:
         c.close()
 
