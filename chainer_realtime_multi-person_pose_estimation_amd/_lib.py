@@ -28,6 +28,8 @@ EXPORTED = (
     "op_set_conv_algo", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect",
+    "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
+    "op_train_enable_layer", "op_train_step",
 )
 ARCH = {"facenet": 1, "handnet": 2}
 MAX_SCALES = 8
@@ -115,6 +117,13 @@ def lib():
         "op_cpm_forward": ([P, P, I32, I32, I32, P], ctypes.c_int),
         "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
+        "op_train_create": ([I32, I32, I32, I32, P], ctypes.c_int),
+        "op_train_destroy": ([P], ctypes.c_int),
+        "op_train_set_weights": ([P, P, P], ctypes.c_int),
+        "op_train_get_weights": ([P, P, P, P, P], ctypes.c_int),
+        "op_train_set_hyper": ([P, D, D, D, D], ctypes.c_int),
+        "op_train_enable_layer": ([P, I32, I32], ctypes.c_int),
+        "op_train_step": ([P, P, P, P, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -514,3 +523,70 @@ class CpmContext(object):
         check(lib().op_cpm_detect(self.h, ptr(img), h, w, w * 3, float(thresh), int(bool(flip_maps)), ptr(kp),
                                   ptr(found)), "op_cpm_detect")
         return self._keypoints(kp, found)
+
+
+class TrainContext(object):
+    """Owns one op_train_ctx: CocoPoseNet master weights, Adam state and the activations of a batch
+    of n frames of h x w on one device (train_coco_pose_estimation.py's Updater on the GPU)."""
+
+    def __init__(self, n, h, w, device=0):
+        self.n, self.h, self.w = int(n), int(h), int(w)
+        self.table = layer_table()
+        hdl = ctypes.c_void_p()
+        check(lib().op_train_create(int(device), self.n, self.h, self.w, ctypes.byref(hdl)), "op_train_create")
+        self.h_ = hdl
+
+    def close(self):
+        if getattr(self, "h_", None) is not None and self.h_.value:
+            lib().op_train_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_weights(self, weights):
+        Ws, bs = [], []
+        for name, ci, co, k in self.table:
+            W, b = weights[name]
+            W = np.ascontiguousarray(W, np.float32)
+            b = np.ascontiguousarray(b, np.float32)
+            if W.shape != (co, ci, k, k) or b.shape != (co,):
+                raise ValueError("%s: expected W %s, got %s" % (name, (co, ci, k, k), W.shape))
+            Ws.append(W)
+            bs.append(b)
+        Wp = (ctypes.c_void_p * len(Ws))(*[a.ctypes.data for a in Ws])
+        bp = (ctypes.c_void_p * len(bs))(*[a.ctypes.data for a in bs])
+        check(lib().op_train_set_weights(self.h_, Wp, bp), "op_train_set_weights")
+
+    def get(self, grads=False):
+        """{layer: (W, b)} of the current weights, or of the last step's (unscaled) gradients."""
+        out = {name: (np.empty((co, ci, k, k), np.float32), np.empty(co, np.float32))
+               for name, ci, co, k in self.table}
+        Wp = (ctypes.c_void_p * len(self.table))(*[out[t[0]][0].ctypes.data for t in self.table])
+        bp = (ctypes.c_void_p * len(self.table))(*[out[t[0]][1].ctypes.data for t in self.table])
+        args = (None, None, Wp, bp) if grads else (Wp, bp, None, None)
+        check(lib().op_train_get_weights(self.h_, *args), "op_train_get_weights")
+        return out
+
+    def set_hyper(self, alpha, beta1=0.9, beta2=0.999, eps=1e-8):
+        check(lib().op_train_set_hyper(self.h_, float(alpha), float(beta1), float(beta2), float(eps)),
+              "op_train_set_hyper")
+
+    def enable(self, layer_index, on=True):
+        check(lib().op_train_enable_layer(self.h_, int(layer_index), int(bool(on))), "op_train_enable_layer")
+
+    def step(self, x, pafs_t, heatmaps_t, ignore_mask):
+        n, h8, w8 = self.n, self.h // 8, self.w // 8
+        x = np.ascontiguousarray(x, np.float32)
+        pt = np.ascontiguousarray(pafs_t, np.float32)
+        ht = np.ascontiguousarray(heatmaps_t, np.float32)
+        ig = np.ascontiguousarray(ignore_mask, np.uint8)
+        if x.shape != (n, 3, self.h, self.w) or pt.shape != (n, 38, h8, w8) or ht.shape != (n, 19, h8, w8) \
+                or ig.shape != (n, h8, w8):
+            raise ValueError("train step: shapes (n,3,h,w) (n,38,h/8,w/8) (n,19,h/8,w/8) (n,h/8,w/8) expected")
+        losses = np.zeros(12, np.float64)
+        check(lib().op_train_step(self.h_, ptr(x), ptr(pt), ptr(ht), ptr(ig), ptr(losses)), "op_train_step")
+        return losses

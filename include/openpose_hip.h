@@ -244,6 +244,28 @@ int op_cpm_peaks(op_cpm_ctx* ctx, const float* heatmaps, int32_t c, int32_t h, i
 int op_cpm_detect(op_cpm_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, float thresh,
                   int32_t flip_maps, double* keypoints, int32_t* found);
 
+/* ---- Training iteration: Updater.update_core of train_coco_pose_estimation.py:93-123 ----
+ * One context = CocoPoseNet master weights (f32), Adam state and every activation of a batch of n
+ * frames of h x w (multiples of 8) on one device.  Exact f32 (v_mfma_f32_32x32x2_f32 forward and
+ * input-gradient convs).  Layers in op_layer_info order. */
+typedef struct op_train_ctx op_train_ctx;
+int op_train_create(int32_t device, int32_t n, int32_t h, int32_t w, op_train_ctx** out);
+int op_train_destroy(op_train_ctx* ctx);
+/* initmodel / copy_vgg_params (:183-189): weights + biases; resets the Adam state. */
+int op_train_set_weights(op_train_ctx* ctx, const float* const* W, const float* const* b);
+/* Current weights / biases and the last step's (unscaled) gradients; any array may be null. */
+int op_train_get_weights(op_train_ctx* ctx, float* const* W, float* const* b, float* const* gW, float* const* gb);
+/* optimizers.Adam(alpha, beta1, beta2, eps) (:214); the caller's alpha schedule (:104-107) sets alpha. */
+int op_train_set_hyper(op_train_ctx* ctx, double alpha, double beta1, double beta2, double eps);
+/* enable_update / disable_update of one layer (:225-230, :97-102). */
+int op_train_enable_layer(op_train_ctx* ctx, int32_t layer, int32_t enable);
+/* One iteration: x = preprocess(imgs) (n, 3, h, w) f32; pafs_t (n, 38, h/8, w/8), heat_t (n, 19, h/8,
+ * w/8) f32; ignore (n, h/8, w/8) u8 (1 = ignored); losses[12] = per stage (paf, heat) MSE of
+ * compute_loss (:42-77).  Forward, loss, backward, GradientScaling(1/4) on conv1_1 .. conv4_4_CPM,
+ * Adam on the enabled layers. */
+int op_train_step(op_train_ctx* ctx, const float* x, const float* pafs_t, const float* heat_t, const uint8_t* ignore,
+                  double* losses);
+
 #ifdef __cplusplus
 }
 #endif
