@@ -27,7 +27,9 @@ constexpr int kP1R = 8, kP1C = 32;                 // conv1_2 tile
 constexpr int kP1HR = kP1R + 2, kP1HC = kP1C + 2;  // conv1_1 window = conv1_2 halo (pitch kP1HC)
 constexpr int kP1IR = kP1R + 4, kP1IC = kP1C + 4;  // network-input window
 constexpr int kP1Slots = kP1HR * kP1HC;            // 340
-constexpr int kP1Plane = kP1Slots * 16;            // bytes per plane
+// bytes per plane, a multiple of 256 so all 8 planes start on bank 0: a ds_read_b128 lane group
+// spans two planes (k-halves), and with a 64-B plane offset their 16-B slots collided (2-way)
+constexpr int kP1Plane = (kP1Slots * 16 + 255) / 256 * 256;  // (no measurable change in an A/B)
 constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
 
 __device__ __forceinline__ float p1_recon(float v) {
