@@ -92,7 +92,7 @@ MFMA_7X7 = {4: "v_mfma_f32_16x16x32_bf16", 5: "v_mfma_f32_16x16x32_bf16", 6: "v_
 
 def committed_traffic(kernel, batch, precision, halo_mode):
     """HBM bytes per launch (read + write) of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/*_traffic.json, FETCH_SIZE x2 + WRITE_SIZE, tools/summarize_profile.py) taken
+    summary (profiles/*_traffic.json, FETCH_SIZE x calibrated pattern factor + WRITE_SIZE, tools/summarize_profile.py) taken
     on this exact workload; (None, None) when no profile matches."""
     import glob
     best = None

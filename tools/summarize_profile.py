@@ -1,8 +1,12 @@
 """Summarise a tools/profile.sh run into profiles/<tag>.md + profiles/<tag>_traffic.json.
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from
-separate --pmc passes (KiB units); on gfx950 FETCH_SIZE reads half the bytes of a wide coalesced
-stream, so it is doubled (an upper-bound correction for the narrower accesses).
+separate --pmc passes (KiB units).  On gfx950 FETCH_SIZE reads half the bytes of a wide coalesced
+16-B/lane stream (the guide's calibration, doubled here by default); the conv kernels' halo loads
+are not streams, so their factor comes from our own calibration on a known byte count
+(tools/micro/fetch_calib.hip, profiles/fetch_calib_r01.md): a 64-B channel chunk of each pixel
+record (conv_m16_bf16x3's 7x7 halo) is counted at x0.98 of its bytes, a 128-B chunk pair
+(conv_m16k_bf16x3's 3x3 halo) at x1.12.
 usage: python tools/summarize_profile.py gpurun_out/prof_<tag> <tag>
 """
 import csv
@@ -27,6 +31,17 @@ def pmc(d, sub, counter):
     return acc
 
 
+# FETCH_SIZE -> bytes, by kernel (dominant read pattern); default: the guide's 16-B/lane stream
+FETCH_FACTOR = (("conv_m16_bf16x3", 536870912 / 545724096), ("conv_m16k_bf16x3", 268435456 / 240281984))
+
+
+def fetch_factor(name):
+    for prefix, f in FETCH_FACTOR:
+        if short(name).replace("op::", "").startswith(prefix):
+            return f
+    return 2.0
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "")
 
@@ -48,17 +63,18 @@ def main():
              "Bench line of the stats pass: value %.1f frames/s, ms/step %.2f, dtype %s, batch %s." % (
                  bench.get("value", 0), bench.get("ms_per_step", 0), bench.get("dtype"),
                  bench.get("config", {}).get("frames_per_step_per_gpu")), "",
-             "| kernel | calls | avg us | total % | HBM read MB/launch (FETCH x2) | HBM write MB/launch |",
+             "| kernel | calls | avg us | total % | HBM read MB/launch (FETCH x calibrated factor) | HBM write MB/launch |",
              "|---|---|---|---|---|---|"]
     traffic = {}
     for r in stats:
         name = r["Name"]
         f = fetch.get(name, [])
         w = write.get(name, [])
-        fr = 2 * 1024 * sum(f) / len(f) / 1e6 if f else None
+        fr = fetch_factor(name) * 1024 * sum(f) / len(f) / 1e6 if f else None
         wr = 1024 * sum(w) / len(w) / 1e6 if w else None
         if fr is not None and wr is not None:
-            traffic[short(name)] = {"read_bytes": fr * 1e6, "write_bytes": wr * 1e6, "avg_ns": float(r["AverageNs"])}
+            traffic[short(name)] = {"read_bytes": fr * 1e6, "write_bytes": wr * 1e6, "avg_ns": float(r["AverageNs"]),
+                                   "fetch_factor": round(fetch_factor(name), 4)}
         lines.append("| `%s` | %s | %.1f | %.2f | %s | %s |" % (
             short(name)[:80], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["Percentage"]),
             "%.1f" % fr if fr is not None else "-", "%.1f" % wr if wr is not None else "-"))
