@@ -27,7 +27,7 @@ EXPORTED = (
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
-    "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect",
+    "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
     "op_train_enable_layer", "op_train_step",
 )
@@ -117,6 +117,7 @@ def lib():
         "op_cpm_forward": ([P, P, I32, I32, I32, P], ctypes.c_int),
         "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
+        "op_cpm_detect_batch": ([P, I32, P, P, P, P, ctypes.c_float, P, P, P], ctypes.c_int),
         "op_train_create": ([I32, I32, I32, I32, P], ctypes.c_int),
         "op_train_destroy": ([P], ctypes.c_int),
         "op_train_set_weights": ([P, P, P], ctypes.c_int),
@@ -523,6 +524,29 @@ class CpmContext(object):
         check(lib().op_cpm_detect(self.h, ptr(img), h, w, w * 3, float(thresh), int(bool(flip_maps)), ptr(kp),
                                   ptr(found)), "op_cpm_detect")
         return self._keypoints(kp, found)
+
+    def detect_batch(self, crops, thresh, flip_maps=None):
+        """``detect`` over a list of BGR crops (any sizes) in one batched forward; the same results
+        as one ``detect`` call per crop."""
+        imgs = [np.ascontiguousarray(c, np.uint8) for c in crops]
+        for img in imgs:
+            if img.ndim != 3 or img.shape[2] != 3:
+                raise ValueError("expected H x W x 3 uint8 BGR crops")
+        n, np_ = len(imgs), self.n_maps - 1
+        if n == 0:
+            return []
+        ptrs = (ctypes.c_void_p * n)(*[img.ctypes.data for img in imgs])
+        hs = np.array([img.shape[0] for img in imgs], np.int32)
+        ws = np.array([img.shape[1] for img in imgs], np.int32)
+        rs = np.array([img.shape[1] * 3 for img in imgs], np.int64)
+        fl = np.array([int(bool(f)) for f in (flip_maps or [False] * n)], np.int32)
+        if len(fl) != n:
+            raise ValueError("flip_maps needs one entry per crop")
+        kp = np.zeros((n, np_, 3), np.float64)
+        found = np.zeros((n, np_), np.int32)
+        check(lib().op_cpm_detect_batch(self.h, n, ptrs, ptr(hs), ptr(ws), ptr(rs), float(thresh), ptr(fl), ptr(kp),
+                                        ptr(found)), "op_cpm_detect_batch")
+        return [self._keypoints(kp[i], found[i]) for i in range(n)]
 
 
 class TrainContext(object):

@@ -550,9 +550,10 @@ int op_cpm_forward(op_cpm_ctx* c, const float* x, int32_t n, int32_t h, int32_t 
   return OP_OK;
 }
 
-// gaussian + argmax over the first c-1 planes of the device maps `heat` (c, h, w) -> host results
-static int cpm_peaks_dev(op_cpm_ctx* c, float* heat, float* tmp, float* filt, int32_t* dres, int ch, int h, int w,
-                         float thresh, int flip, double* kp, int32_t* found) {
+// gaussian + argmax over the first c-1 planes of the device maps `heat` (c, h, w) -> dres
+// (c-1 records of [max bits, count, first two row-major maxima], device)
+static int cpm_peaks_launch(op_cpm_ctx* c, float* heat, float* tmp, float* filt, int32_t* dres, int ch, int h, int w,
+                            int flip) {
   const int np = ch - 1;
   if (np < 1) return OP_OK;
   const int64_t tot = (int64_t)np * h * w;
@@ -564,9 +565,25 @@ static int cpm_peaks_dev(op_cpm_ctx* c, float* heat, float* tmp, float* filt, in
   hipLaunchKernelGGL(cpm_argmax, dim3((unsigned)np), dim3(kArgT), 0, c->stream, filt, h, w, flip, dres);
   OP_AFTER_LAUNCH("cpm_argmax", c->stream);
   OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+static void cpm_peaks_decode(const int32_t* res, int ch, int w, float thresh, double* kp, int32_t* found);
+
+static int cpm_peaks_dev(op_cpm_ctx* c, float* heat, float* tmp, float* filt, int32_t* dres, int ch, int h, int w,
+                         float thresh, int flip, double* kp, int32_t* found) {
+  const int np = ch - 1;
+  if (np < 1) return OP_OK;
+  CRC(cpm_peaks_launch(c, heat, tmp, filt, dres, ch, h, w, flip));
   std::vector<int32_t> res((size_t)np * 4);
   OP_HIP_CHECK(hipMemcpyAsync(res.data(), dres, res.size() * 4, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  cpm_peaks_decode(res.data(), ch, w, thresh, kp, found);
+  return OP_OK;
+}
+
+static void cpm_peaks_decode(const int32_t* res, int ch, int w, float thresh, double* kp, int32_t* found) {
+  const int np = ch - 1;
   for (int i = 0; i < np; ++i) {
     float m;
     memcpy(&m, &res[4 * i], 4);
@@ -584,7 +601,6 @@ static int cpm_peaks_dev(op_cpm_ctx* c, float* heat, float* tmp, float* filt, in
     k[1] = (double)y0;                                // coords[0]
     k[2] = (double)m;
   }
-  return OP_OK;
 }
 
 int op_cpm_peaks(op_cpm_ctx* c, const float* heatmaps, int32_t ch, int32_t h, int32_t w, float thresh, int32_t flip,
@@ -632,6 +648,67 @@ int op_cpm_detect(op_cpm_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   CRC(launch_resize_images(low, ch, lh, lw, h, w, heat, c->stream));
   return cpm_peaks_dev(c, heat, (float*)(s + ib + lb + pb), (float*)(s + ib + lb + 2 * pb),
                        (int32_t*)(s + ib + lb + 3 * pb), ch, h, w, thresh, flip_maps, keypoints, found);
+}
+
+int op_cpm_detect_batch(op_cpm_ctx* c, int32_t n, const uint8_t* const* bgr, const int32_t* h, const int32_t* w,
+                        const int64_t* row_stride, float thresh, const int32_t* flip_maps, double* keypoints,
+                        int32_t* found) {
+  CRC(cpm_check(c, true));
+  if (n < 0 || (n > 0 && (!bgr || !h || !w || !row_stride || !keypoints || !found))) {
+    set_error("op_cpm_detect_batch: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  for (int i = 0; i < n; ++i)
+    if (!bgr[i] || h[i] < 2 || w[i] < 2 || row_stride[i] < (int64_t)w[i] * 3 || (int64_t)h[i] * w[i] >= (1ll << 31)) {
+      set_error("op_cpm_detect_batch: bad crop " + std::to_string(i));
+      return OP_ERR_INVALID;
+    }
+  if (n == 0) return OP_OK;
+  const int S = 368;  // as op_cpm_detect
+  CRC(cpm_geometry(c, n, S, S));
+  const int lh = S / 8, lw = S / 8, ch = c->nm, np = ch - 1;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  // scratch: every crop's bytes, the batch's low-resolution maps, one full-size heat / tmp / filt
+  // set (the per-crop upsample + peak launches run in stream order), the argmax records
+  std::vector<size_t> ioff(n);
+  size_t off = 0, pb = 0;
+  for (int i = 0; i < n; ++i) {
+    ioff[i] = off;
+    off += al((size_t)h[i] * row_stride[i]);
+    pb = std::max(pb, al((size_t)ch * h[i] * w[i] * 4));
+  }
+  const size_t lb = al((size_t)n * ch * lh * lw * 4);
+  const size_t low_off = off, heat_off = off + lb;
+  const size_t res_off = heat_off + 3 * pb;
+  CRC(cpm_scratch(c, res_off + (size_t)n * std::max(np, 1) * 16));
+  char* s = (char*)c->scratch;
+  const size_t fx = c->buf[X0].floats(1);
+  for (int i = 0; i < n; ++i) {
+    OP_HIP_CHECK(hipMemcpyAsync(s + ioff[i], bgr[i], (size_t)h[i] * row_stride[i], hipMemcpyHostToDevice, c->stream));
+    CRC(launch_preprocess_split((const uint8_t*)(s + ioff[i]), 0, row_stride[i], 1, h[i], w[i], S, S,
+                                c->buf[X0].p + (size_t)i * fx, c->stream, 256.0f));
+  }
+  CRC(cpm_run(c));
+  float* low = (float*)(s + low_off);
+  const int64_t tot = (int64_t)n * ch * lh * lw;
+  hipLaunchKernelGGL(cpm_planar, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->buf[MAP32].p,
+                     c->buf[MAP32].cs, ch, n, lh * lw, low);
+  OP_AFTER_LAUNCH("cpm_planar", c->stream);
+  float* heat = (float*)(s + heat_off);
+  int32_t* dres = (int32_t*)(s + res_off);
+  for (int i = 0; i < n; ++i) {
+    CRC(launch_resize_images(low + (size_t)i * ch * lh * lw, ch, lh, lw, h[i], w[i], heat, c->stream));
+    CRC(cpm_peaks_launch(c, heat, (float*)(s + heat_off + pb), (float*)(s + heat_off + 2 * pb),
+                         dres + (size_t)i * np * 4, ch, h[i], w[i], flip_maps ? flip_maps[i] : 0));
+  }
+  if (np < 1) return OP_OK;
+  std::vector<int32_t> res((size_t)n * np * 4);
+  OP_HIP_CHECK(hipMemcpyAsync(res.data(), dres, res.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < n; ++i)
+    cpm_peaks_decode(res.data() + (size_t)i * np * 4, ch, w[i], thresh, keypoints + (size_t)i * np * 3,
+                     found + (size_t)i * np);
+  return OP_OK;
 }
 
 }  // extern "C"

@@ -36,24 +36,32 @@ def draw_rectangle(img, p0, p1, color):
 
 
 def run(img, pose_detector, face_detector, hand_detector, log=print):
+    """demo.py:20-56.  The crops of every person are detected in two batched forwards (faces,
+    hands: ``detect_batch``) and drawn in the reference's per-person order, so the image is the
+    same as with one detector call per crop."""
     log("Estimating pose...")
     person_pose_array, _ = pose_detector(img)
     res_img = add_weighted(img, 0.6, draw_person_pose(img, person_pose_array), 0.4, 0)
+    faces, hands = [], []
     for person_pose in person_pose_array:
         unit_length = pose_detector.get_unit_length(person_pose)
+        faces.append(pose_detector.crop_face(img, person_pose, unit_length))
+        hands.append(pose_detector.crop_hands(img, person_pose, unit_length))
+    face_crops = [f[0] for f in faces if f[0] is not None]
+    hand_crops = [(h[side]["img"], side) for h in hands for side in ("left", "right") if h[side] is not None]
+    face_kps = iter(face_detector.detect_batch(face_crops) if face_crops else [])
+    hand_kps = iter(hand_detector.detect_batch([c for c, _ in hand_crops], [s for _, s in hand_crops])
+                    if hand_crops else [])
+    for (cropped_face_img, bbox), person_hands in zip(faces, hands):
         log("Estimating face keypoints...")
-        cropped_face_img, bbox = pose_detector.crop_face(img, person_pose, unit_length)
         if cropped_face_img is not None:
-            face_keypoints = face_detector(cropped_face_img)
-            res_img = draw_face_keypoints(res_img, face_keypoints, (bbox[0], bbox[1]))
+            res_img = draw_face_keypoints(res_img, next(face_kps), (bbox[0], bbox[1]))
             draw_rectangle(res_img, (bbox[0], bbox[1]), (bbox[2], bbox[3]), (255, 255, 255))
         log("Estimating hands keypoints...")
-        hands = pose_detector.crop_hands(img, person_pose, unit_length)
         for side in ("left", "right"):
-            if hands[side] is not None:
-                hand_img, bbox = hands[side]["img"], hands[side]["bbox"]
-                hand_keypoints = hand_detector(hand_img, hand_type=side)
-                res_img = draw_hand_keypoints(res_img, hand_keypoints, (bbox[0], bbox[1]))
+            if person_hands[side] is not None:
+                bbox = person_hands[side]["bbox"]
+                res_img = draw_hand_keypoints(res_img, next(hand_kps), (bbox[0], bbox[1]))
                 draw_rectangle(res_img, (bbox[0], bbox[1]), (bbox[2], bbox[3]), (255, 255, 255))
     return res_img
 

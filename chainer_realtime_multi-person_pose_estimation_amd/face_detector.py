@@ -46,6 +46,10 @@ class FaceDetector(object):
     def __call__(self, face_img, fast_mode=False):
         return self._ctx.detect(face_img, params["face_heatmap_peak_thresh"])
 
+    def detect_batch(self, face_imgs):
+        """``__call__`` over many crops in one batched forward (op_cpm_detect_batch)."""
+        return self._ctx.detect_batch(face_imgs, params["face_heatmap_peak_thresh"])
+
 
 def draw_face_keypoints(orig_img, face_keypoints, left_top):
     """face_detector.py:86-102: radius-2 discs and 1-px lines in (255, 255, 0) (BGR)."""

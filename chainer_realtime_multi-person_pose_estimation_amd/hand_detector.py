@@ -46,6 +46,13 @@ class HandDetector(object):
             hand_img = np.ascontiguousarray(np.asarray(hand_img)[:, ::-1])
         return self._ctx.detect(hand_img, params["hand_heatmap_peak_thresh"], flip_maps=left)
 
+    def detect_batch(self, hand_imgs, hand_types):
+        """``__call__`` over many crops in one batched forward (op_cpm_detect_batch): the same
+        keypoints as one call per crop, for demo.py's every-person loop."""
+        lefts = [t == "left" for t in hand_types]
+        imgs = [np.ascontiguousarray(np.asarray(im)[:, ::-1]) if lf else im for im, lf in zip(hand_imgs, lefts)]
+        return self._ctx.detect_batch(imgs, params["hand_heatmap_peak_thresh"], flip_maps=lefts)
+
 
 def draw_hand_keypoints(orig_img, hand_keypoints, left_top):
     """hand_detector.py:96-116: per finger, radius-3 discs on both ends and a 1-px line."""

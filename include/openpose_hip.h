@@ -243,6 +243,13 @@ int op_cpm_peaks(op_cpm_ctx* ctx, const float* heatmaps, int32_t c, int32_t h, i
  * keypoints (c-1, 3) f64, found (c-1,). */
 int op_cpm_detect(op_cpm_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, float thresh,
                   int32_t flip_maps, double* keypoints, int32_t* found);
+/* op_cpm_detect over n crops of any sizes in one batched forward (demo.py:38-56's per-person face /
+ * hand calls, which the reference makes one at a time): crop i = bgr[i] (h[i] x w[i] x 3 u8, row
+ * stride row_stride[i]), flip_maps[i] as above (may be NULL: none).  Results are identical to n
+ * op_cpm_detect calls: keypoints (n, c-1, 3) f64, found (n, c-1). */
+int op_cpm_detect_batch(op_cpm_ctx* ctx, int32_t n, const uint8_t* const* bgr, const int32_t* h, const int32_t* w,
+                        const int64_t* row_stride, float thresh, const int32_t* flip_maps, double* keypoints,
+                        int32_t* found);
 
 /* ---- Training iteration: Updater.update_core of train_coco_pose_estimation.py:93-123 ----
  * One context = CocoPoseNet master weights (f32), Adam state and every activation of a batch of n

@@ -79,6 +79,25 @@ def test_cpm_detect_equals_oracle_composition(cpm, hw, hand_type):
     _same(got, exp)
 
 
+def test_cpm_detect_batch_equals_single_calls(cpm):
+    """op_cpm_detect_batch over crops of mixed sizes (and mixed left/right readouts) == one
+    op_cpm_detect per crop, bit for bit."""
+    arch, c, _ = cpm
+    rng = np.random.default_rng(11)
+    sizes = [(96, 80), (61, 75), (300, 210), (40, 33), (368, 368)]
+    crops = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in sizes]
+    flips = [arch == "handnet" and i % 2 == 1 for i in range(len(crops))]
+    for thr in (-10.0, 0.05):
+        single = [c.detect(im, thr, flip_maps=f) for im, f in zip(crops, flips)]
+        batch = c.detect_batch(crops, thr, flip_maps=flips)
+        assert len(batch) == len(single)
+        for g, e in zip(batch, single):
+            _same(g, e)
+    assert c.detect_batch([], 0.1) == []
+    with pytest.raises(ValueError):
+        c.detect_batch([crops[0], crops[1][:1]], 0.1)  # a 1-row crop: rejected like op_cpm_detect
+
+
 def test_face_and_hand_detector_api():
     fd = pkg_module("face_detector").FaceDetector("facenet", None, model=pkg_module("weights").random_weights(1, arch="facenet"))
     hd = pkg_module("hand_detector").HandDetector("handnet", None, model=pkg_module("weights").random_weights(1, arch="handnet"))
@@ -115,6 +134,22 @@ def test_demo_on_golden_poses(tmp_path):
     out = demo.run(img, Pose(), fd, hd, log=log.append)
     assert out.shape == img.shape and out.dtype == np.uint8 and (out != img).any()
     assert log.count("Estimating face keypoints...") == len(poses)
+    # the batched detectors draw the same image as the reference's one call per crop
+    seq = demo.add_weighted(img, 0.6, pkg_module("draw").draw_person_pose(img, poses), 0.4, 0)
+    for pose in poses:
+        unit = pd.get_unit_length(pose)
+        face, bbox = pd.crop_face(img, pose, unit)
+        if face is not None:
+            seq = pkg_module("face_detector").draw_face_keypoints(seq, fd(face), (bbox[0], bbox[1]))
+            demo.draw_rectangle(seq, (bbox[0], bbox[1]), (bbox[2], bbox[3]), (255, 255, 255))
+        hands = pd.crop_hands(img, pose, unit)
+        for side in ("left", "right"):
+            if hands[side] is not None:
+                bbox = hands[side]["bbox"]
+                seq = pkg_module("hand_detector").draw_hand_keypoints(seq, hd(hands[side]["img"], hand_type=side),
+                                                                      (bbox[0], bbox[1]))
+                demo.draw_rectangle(seq, (bbox[0], bbox[1]), (bbox[2], bbox[3]), (255, 255, 255))
+    assert np.array_equal(out, seq)
     # the CLI with seeded random weights (no persons: the pose blend only)
     dst = tmp_path / "result.png"
     src = os.path.join(GOLDEN, "people.png")
