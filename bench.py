@@ -216,14 +216,13 @@ def main():
                                     for i, r in enumerate(res)], 64)
             Fr.gather_records(recs, 64, device=coll_dev)
 
-    # timed region: HIP events only around the dominant kernel (the 7x7 stage convs) for the
-    # roofline, so the per-launch event overhead stays off the other ~90 launches of a step; set
-    # before the warmup so a step graph is captured (with its event-record nodes) outside the timing
-    ctx.profile_classes(["conv7x7"])
-    ctx.profile(not args.no_profile)
     for _ in range(args.warmup):
         step(False)
     ctx.synchronize()
+    # timed region: HIP events only around the dominant kernel (the 7x7 stage convs) for the
+    # roofline, so the per-launch event overhead stays off the other ~90 launches of a step
+    ctx.profile_classes(["conv7x7"])
+    ctx.profile(not args.no_profile and not args.graph)
     ctx.profile_reset()
     barrier()
     t0 = time.perf_counter()

@@ -1406,6 +1406,17 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     if (s.halo_mode != 9 && s.halo_mode != 10 && s.halo_mode != 11 &&
         raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
+      // small launches (one face / hand crop, a single 368x368 frame: 4-8 workgroups of 640 px
+      // for 256 CUs) take 128-px tiles (2 blocks per wave) instead: 5x the workgroups
+      static const int small_below = getenv("OP_M16_SMALL") ? atoi(getenv("OP_M16_SMALL")) : 64;  // tuning aid
+      bool small = false;
+      if (tl.units * tl.per_unit < small_below) {
+        BigTiling ts{};
+        if (raster_tiling(BigConfig{7, 1, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, ts, true)) {
+          tl = ts;
+          small = true;
+        }
+      }
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       static bool attr = false;
@@ -1415,12 +1426,16 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
                                          160 * 1024));
         OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 10, true>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024));
         attr = true;
       }
       const int lds = 4 * 4 * 128 * 16 + 4 * tl.nh * 1024;
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
-      if (pf)
+      if (small)
+        hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), dim3(blocks), dim3(512), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], tl);
+      else if (pf)
         hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), dim3(blocks), dim3(512), lds, st, s, g[0],
                            s.groups > 1 ? g[1] : g[0], tl);
       else

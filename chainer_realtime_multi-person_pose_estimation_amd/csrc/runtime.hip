@@ -286,13 +286,7 @@ struct op_ctx {
   // graph
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
-  uintptr_t g_key[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  // event pairs captured into the graph as external event-record nodes (re-recorded by every
-  // replay); g_pending: a profiled replay whose pairs are not yet accumulated
-  bool capturing = false;
-  std::vector<hipEvent_t> g_events;
-  std::vector<op::ProfPair> g_pairs;
-  bool g_pending = false;
+  uintptr_t g_key[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // multi-scale path: per-scale map intermediates and the running sums over scales
   float* d_pmid = nullptr;
   size_t pmid_bytes = 0;
@@ -519,18 +513,6 @@ static hipEvent_t pool_event(op_ctx* c) {
 template <class Fn>
 static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
   if (!c->prof || !((c->prof_mask >> cls) & 1)) return fn();
-  if (c->capturing) {  // graph capture: external record nodes, timestamped on every replay
-    hipEvent_t a = nullptr, b = nullptr;
-    OP_HIP_CHECK(hipEventCreate(&a));
-    c->g_events.push_back(a);
-    OP_HIP_CHECK(hipEventCreate(&b));
-    c->g_events.push_back(b);
-    OP_HIP_CHECK(hipEventRecordWithFlags(a, c->stream, hipEventRecordExternal));
-    const int rc = fn();
-    OP_HIP_CHECK(hipEventRecordWithFlags(b, c->stream, hipEventRecordExternal));
-    c->g_pairs.push_back(ProfPair{cls, a, b, flops, bytes});
-    return rc;
-  }
   hipEvent_t a = pool_event(c), b = pool_event(c);
   if (!a || !b) return fn();
   OP_HIP_CHECK(hipEventRecord(a, c->stream));
@@ -538,21 +520,6 @@ static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
   OP_HIP_CHECK(hipEventRecord(b, c->stream));
   c->pending.push_back(ProfPair{cls, a, b, flops, bytes});
   return rc;
-}
-
-// Accumulate the event pairs of the last profiled graph replay (the stream must be idle).
-static int resolve_graph_pairs(op_ctx* c) {
-  if (!c->g_pending) return OP_OK;
-  c->g_pending = false;
-  for (const ProfPair& p : c->g_pairs) {
-    float t = 0.0f;
-    OP_HIP_CHECK(hipEventElapsedTime(&t, p.a, p.b));
-    c->prof_ms[p.cls] += t;
-    c->prof_n[p.cls] += 1;
-    c->prof_flops[p.cls] += p.flops;
-    c->prof_bytes[p.cls] += p.bytes;
-  }
-  return OP_OK;
 }
 
 static int conv_class(int ks) { return ks == 7 ? 0 : (ks == 3 ? 1 : 2); }
@@ -1041,7 +1008,6 @@ int op_destroy(op_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
-  for (hipEvent_t e : c->g_events) hipEventDestroy(e);
   free_weights(c);
   for (auto& e : c->arenas) {
     guard_forget(e.p, e.bytes);
@@ -1572,15 +1538,9 @@ int op_run_staged_graph(op_ctx* c) {
   RC(ensure_geometry(c, c->st_n, in_h, in_w));
   RC(ensure_post(c, c->st_n, map_h, map_w));
   // the graph bakes in every pointer and size: replay only if none changed since capture
-  // (and the profiling state: profiled classes are captured as external event-record nodes)
-  const uintptr_t key[11] = {(uintptr_t)c->st_n, (uintptr_t)c->st_h, (uintptr_t)c->st_w, (uintptr_t)c->use_maps,
+  const uintptr_t key[10] = {(uintptr_t)c->st_n, (uintptr_t)c->st_h, (uintptr_t)c->st_w, (uintptr_t)c->use_maps,
                              (uintptr_t)c->arena, (uintptr_t)c->post_arena, (uintptr_t)c->d_frames,
-                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw) * 2 + (uintptr_t)c->split,
-                             (uintptr_t)(c->prof ? 0x10 | c->prof_mask : 0)};
-  if (c->g_pending) {  // the previous replay's events are re-recorded by this one: read them first
-    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-    RC(resolve_graph_pairs(c));
-  }
+                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw) * 2 + (uintptr_t)c->split};
   if (c->gexec && memcmp(key, c->g_key, sizeof(key)) != 0) {
     hipGraphExecDestroy(c->gexec);
     c->gexec = nullptr;
@@ -1588,17 +1548,15 @@ int op_run_staged_graph(op_ctx* c) {
   if (!c->gexec) {
     OP_HIP_CHECK(hipStreamSynchronize(c->stream));
     memcpy(c->g_key, key, sizeof(key));
+    const bool prof = c->prof;
+    c->prof = false;  // no event records inside the capture
     if (c->graph) {
       hipGraphDestroy(c->graph);
       c->graph = nullptr;
     }
-    for (hipEvent_t e : c->g_events) hipEventDestroy(e);
-    c->g_events.clear();
-    c->g_pairs.clear();
     OP_HIP_CHECK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    c->capturing = true;
     int rc = enqueue_staged(c, false);
-    c->capturing = false;
+    c->prof = prof;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (rc) {
@@ -1616,7 +1574,6 @@ int op_run_staged_graph(op_ctx* c) {
   }
   if (getenv("OP_GRAPH_DRYRUN")) return enqueue_staged(c, false);  // debugging aid: eager instead of replay
   OP_HIP_CHECK(hipGraphLaunch(c->gexec, c->stream));
-  c->g_pending = c->prof && !c->g_pairs.empty();
   c->timed = false;
   return OP_OK;
 }
@@ -1625,7 +1582,6 @@ int op_synchronize(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, false));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-  RC(resolve_graph_pairs(c));
   RC(guard_check("op_synchronize"));
   return OP_OK;
 }
@@ -1952,7 +1908,6 @@ int op_profile_reset(op_ctx* c) {
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   c->pending.clear();
   c->ev_used = 0;
-  c->g_pending = false;
   for (int i = 0; i < 4; ++i) {
     c->prof_ms[i] = c->prof_flops[i] = c->prof_bytes[i] = 0.0;
     c->prof_n[i] = 0;
@@ -1968,7 +1923,6 @@ int op_profile_read(op_ctx* c, int32_t cls, double* ms, int64_t* launches, doubl
     return OP_ERR_INVALID;
   }
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-  RC(resolve_graph_pairs(c));
   for (const ProfPair& p : c->pending) {
     float t = 0.0f;
     OP_HIP_CHECK(hipEventElapsedTime(&t, p.a, p.b));
