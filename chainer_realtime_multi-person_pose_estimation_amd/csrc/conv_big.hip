@@ -1119,7 +1119,8 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 // ---- host side ----
 struct BigConfig {
   int ks, npb, nwave, cw, pair, db = 0, raster = 0, wreg = 0;
-  int cap() const { return (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
+  int cap_px = 0;  // pixels per tile when npb does not express it (conv_m16 with an odd block count)
+  int cap() const { return cap_px ? cap_px : (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
   int ring_bytes() const { return wreg ? 0 : (pair ? ((raster || ks == 3) ? 4 : 6) : (db ? 2 : 3)) * 4 * cw * 16; }
   int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
   int halo_budget() const { return (lds_budget() - ring_bytes()) / (db ? 2 : 1); }
@@ -1406,15 +1407,32 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     if (s.halo_mode != 9 && s.halo_mode != 10 && s.halo_mode != 11 &&
         raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
-      // small launches (one face / hand crop, a single 368x368 frame: 4-8 workgroups of 640 px
-      // for 256 CUs) take 128-px tiles (2 blocks per wave) instead: 5x the workgroups
-      static const int small_below = getenv("OP_M16_SMALL") ? atoi(getenv("OP_M16_SMALL")) : 64;  // tuning aid
-      bool small = false;
-      if (tl.units * tl.per_unit < small_below) {
-        BigTiling ts{};
-        if (raster_tiling(BigConfig{7, 1, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, ts, true)) {
-          tl = ts;
-          small = true;
+      // Tile size for launches that leave CUs idle.  A workgroup's time grows as ~(2 + NPX) (fixed
+      // halo / weight-ring / barrier work plus NPX 16-px blocks per wave; measured 0.17 / 0.25 /
+      // 0.50 ms for NPX 2 / 4 / 10), one workgroup per CU, so a launch costs
+      // rounds x (2 + NPX) with rounds = workgroups per XCD / 32 CUs, rounded up.  640-px tiles
+      // (NPX 10) stay whenever they come close to filling the chip (the 38-frame batch: 252);
+      // otherwise the cheapest of NPX 8, 6, 5, 4, 3, 2 (one crop: 2; 16 frames: 5 -> 212
+      // workgroups in one round instead of 106 at 2.4x the work each).
+      static const int force = getenv("OP_M16_NPX") ? atoi(getenv("OP_M16_NPX")) : 0;  // A/B aid
+      auto rounds = [](const BigTiling& t) -> int {
+        return t.xpu ? ((t.per_unit + t.xpu - 1) / t.xpu + 31) / 32 : (t.units * t.per_unit + 255) / 256;
+      };
+      int npx = 10;
+      if (force != 10 && (force || tl.units * tl.per_unit < 230)) {
+        int best = rounds(tl) * (2 + 10);
+        for (int cand : {8, 6, 5, 4, 3, 2}) {
+          if (force && cand != force) continue;
+          BigConfig k{7, 1, 8, 128, 1, 0, 1};
+          k.cap_px = 64 * cand;
+          BigTiling tc{};
+          if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
+          const int cost = rounds(tc) * (2 + cand);
+          if (force || cost < best) {
+            best = cost;
+            npx = cand;
+            tl = tc;
+          }
         }
       }
       if (plain_order) tl.xpu = 0;
@@ -1422,24 +1440,31 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       static bool attr = false;
       static const bool pf = getenv("OP_M16_PF") && atoi(getenv("OP_M16_PF")) != 0;
       if (!attr) {
-        OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 10>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         160 * 1024));
-        OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 10, true>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16_bf16x3<7, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         160 * 1024));
+        const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 10, true>,
+                             (const void*)conv_m16_bf16x3<7, 8>,  (const void*)conv_m16_bf16x3<7, 6>,
+                             (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
+                             (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>};
+        for (const void* f : fns)
+          OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
       const int lds = 4 * 4 * 128 * 16 + 4 * tl.nh * 1024;
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
-      if (small)
-        hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), dim3(blocks), dim3(512), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], tl);
-      else if (pf)
-        hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), dim3(blocks), dim3(512), lds, st, s, g[0],
-                           s.groups > 1 ? g[1] : g[0], tl);
-      else
-        hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), dim3(blocks), dim3(512), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], tl);
+      const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+      switch (npx) {
+        case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 5: hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 4: hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 3: hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 2: hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        default:
+          if (pf)
+            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl);
+          else
+            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl);
+      }
       OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
       OP_HIP_CHECK(hipGetLastError());
       return OP_OK;

@@ -153,6 +153,19 @@ def test_conv_algos_agree(ctx, algo):
         assert err <= FWD_TOL, (algo, shape, err)
 
 
+def test_forward_7x7_tile_sizes_agree(ctx):
+    """The 7x7 raster kernel picks 640-, 256- or 128-px tiles by how many workgroups a launch
+    gets (batch 16 at 368x368: 256-px; one frame: 128-px); the per-pixel MFMA accumulation order
+    does not depend on the tile, so a frame's maps match between batch 16 and batch 1."""
+    rng = np.random.default_rng(16)
+    x = rng.uniform(-0.5, 0.5, (16, 3, 368, 368)).astype(np.float32)
+    pb, hb = ctx.forward(x)
+    for i in (0, 7, 15):
+        p1, h1 = ctx.forward(x[i:i + 1])
+        err = max(float(np.abs(pb[i] - p1[0]).max()), float(np.abs(hb[i] - h1[0]).max()))
+        assert err <= 1e-6, (i, err)
+
+
 def test_forward_precisions_agree(ctx, rand_weights):
     """bf16x3 vs exact-f32 MFMA on a 720p-shaped input (656x368), batch 2."""
     rng = np.random.default_rng(2)
