@@ -197,9 +197,11 @@ __global__ __launch_bounds__(256) void tr_loss(TView Y, int yoff, TView dY, cons
 
 // weight gradient partials: workgroup = 64 co x 64 ci of one tap over the pixel range of split z;
 // thread = 4 co x 4 ci; 16-pixel steps staged in LDS.  part[z][tap][co][ci] (co, ci < cop, cip).
+// The centre tap's first ci block also sums the staged G rows: bias partials bpart[z][co].
 constexpr int kWgPx = 16;
 __global__ __launch_bounds__(256) void tr_wgrad(TView G, int gch, TView X, int n, int cop, int cip, int ks,
-                                                int px_per_split, float* __restrict__ part) {
+                                                int px_per_split, float* __restrict__ part,
+                                                float* __restrict__ bpart) {
   __shared__ float sg[kWgPx][64];
   __shared__ float sx[kWgPx][64];
   const int co0 = blockIdx.x * 64;
@@ -211,7 +213,9 @@ __global__ __launch_bounds__(256) void tr_wgrad(TView G, int gch, TView X, int n
   const int p0 = z * px_per_split, p1 = min(p0 + px_per_split, total);
   const int tid = threadIdx.x;
   const int tco = (tid & 15) * 4, tci = (tid >> 4) * 4;
+  const bool bwg = tap == taps / 2 && ci0 == 0;  // workgroup-uniform: this one also sums the bias
   float acc[4][4] = {};
+  float bacc = 0.0f;  // bwg, threads 0..63: channel co0 + tid
   for (int pb = p0; pb < p1; pb += kWgPx) {
     // stage 16 px x 64 channels of G and of the shifted X (one float4 per thread each)
     {
@@ -236,8 +240,12 @@ __global__ __launch_bounds__(256) void tr_wgrad(TView G, int gch, TView X, int n
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __fmaf_rn(a[i], b[j], acc[i][j]);
     }
+    if (bwg && tid < 64)
+#pragma unroll
+      for (int k = 0; k < kWgPx; ++k) bacc += sg[k][tid];
     __syncthreads();
   }
+  if (bwg && tid < 64 && co0 + tid < cop) bpart[(int64_t)z * cop + co0 + tid] = bacc;
   float* o = part + ((int64_t)z * taps + tap) * (int64_t)cop * cip;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -246,28 +254,7 @@ __global__ __launch_bounds__(256) void tr_wgrad(TView G, int gch, TView X, int n
       if (co0 + tco + i < cop && ci0 + tci + j < cip) o[(int64_t)(co0 + tco + i) * cip + ci0 + tci + j] = acc[i][j];
 }
 
-// bias gradient partials: part[z][co] = sum over the split's pixels of G[p][co]; workgroup = 64
-// channels x 4 pixel lanes (coalesced 256-B rows), lanes combined in a fixed order
-__global__ __launch_bounds__(256) void tr_bgrad(TView G, int gch, int n, int cop, int px_per_split,
-                                                float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, lane4 = threadIdx.x >> 6;
-  const int co = blockIdx.x * 64 + c;
-  const int z = blockIdx.y;
-  const int hw = G.h * G.w, total = n * hw;
-  const int p0 = z * px_per_split, p1 = min(p0 + px_per_split, total);
-  float s = 0.0f;
-  if (co < gch)
-    for (int p = p0 + lane4; p < p1; p += 4) {
-      const int f = p / hw, r = p - f * hw, y = r / G.w, x = r - y * G.w;
-      s += G.p[G.at(f, y, x) + co];
-    }
-  red[lane4][c] = s;
-  __syncthreads();
-  if (lane4 == 0 && co < cop) part[(int64_t)z * cop + co] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
-}
-
-// gW[co][ci_log][tap] += sum_z part[z][tap][co][ci_phys] (fixed order); cat: physical -> logical
+// gW[co][ci_log][tap] = sum_z part[z][tap][co][ci_phys] (fixed order); cat: physical -> logical
 __global__ __launch_bounds__(256) void tr_wreduce(const float* __restrict__ part, int splits, int taps, int cop, int cip,
                                                   int Co, int Ci, int cat, float* __restrict__ gW) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -287,7 +274,7 @@ __global__ __launch_bounds__(256) void tr_wreduce(const float* __restrict__ part
   if (ci >= Ci) return;
   float s = 0.0f;
   for (int z = 0; z < splits; ++z) s += part[((int64_t)z * taps + tap) * (int64_t)cop * cip + (int64_t)co * cip + pci];
-  gW[((int64_t)co * Ci + ci) * taps + tap] += s;
+  gW[((int64_t)co * Ci + ci) * taps + tap] = s;
 }
 
 __global__ __launch_bounds__(256) void tr_breduce(const float* __restrict__ part, int splits, int cop, int Co,
@@ -296,7 +283,7 @@ __global__ __launch_bounds__(256) void tr_breduce(const float* __restrict__ part
   if (co >= Co) return;
   float s = 0.0f;
   for (int z = 0; z < splits; ++z) s += part[(int64_t)z * cop + co];
-  gb[co] += s;
+  gb[co] = s;
 }
 
 // Chainer AdamRule.update_core (eta 1, no weight decay): grad *= scale (GradientScaling hook);
@@ -609,7 +596,7 @@ int tr_backward(op_train_ctx* c, int lowest) {
       const int cop = c->cop[l], cip = cv.cin_phys;
       const int splits = std::max(1, std::min(64, total / 512));
       const int pps = ((total + splits - 1) / splits + kWgPx - 1) / kWgPx * kWgPx;
-      const size_t need = (size_t)splits * taps * cop * cip;
+      const size_t need = (size_t)splits * taps * cop * cip + (size_t)splits * cop;  // + bias partials
       if (need > c->part_floats) {
         OP_HIP_CHECK(hipStreamSynchronize(c->stream));
         if (c->part) OP_HIP_CHECK(hipFree(c->part));
@@ -621,12 +608,12 @@ int tr_backward(op_train_ctx* c, int lowest) {
       const dim3 grid((unsigned)((cop + 63) / 64), (unsigned)(taps * ((cip + 63) / 64)), (unsigned)splits);
       // (a v_mfma_f32_32x32x2_f32 version with operands straight from L2 measured slower: 154 vs
       // 144 ms per batch-10 iteration)
-      hipLaunchKernelGGL(tr_wgrad, grid, dim3(256), 0, c->stream, gs, cv.store, xv, n, cop, cip, d.k, pps, c->part);
+      float* bpart = c->part + (size_t)splits * taps * cop * cip;
+      hipLaunchKernelGGL(tr_wgrad, grid, dim3(256), 0, c->stream, gs, cv.store, xv, n, cop, cip, d.k, pps, c->part,
+                         bpart);
       hipLaunchKernelGGL(tr_wreduce, dim3(nb((int64_t)taps * cop * cip)), dim3(256), 0, c->stream, c->part, splits,
                          taps, cop, cip, d.co, d.ci, cv.cat ? 1 : 0, c->gW[l]);
-      hipLaunchKernelGGL(tr_bgrad, dim3((unsigned)((cop + 63) / 64), (unsigned)splits), dim3(256), 0, c->stream, gs,
-                         cv.store, n, cop, pps, c->part);
-      hipLaunchKernelGGL(tr_breduce, dim3(nb(d.co)), dim3(256), 0, c->stream, c->part, splits, cop, d.co, c->gb[l]);
+      hipLaunchKernelGGL(tr_breduce, dim3(nb(d.co)), dim3(256), 0, c->stream, bpart, splits, cop, d.co, c->gb[l]);
     }
     if (l > lowest && l > 0) {  // input gradient: temp = conv(dY_pre, W'), then added to the input's gradient
       TView tv = xin;
@@ -801,6 +788,11 @@ int op_train_enable_layer(op_train_ctx* c, int32_t layer, int32_t enable) {
     set_error("op_train_enable_layer: bad layer");
     return OP_ERR_INVALID;
   }
+  if (!enable && c->enabled[layer]) {  // a disabled layer reports zero gradients (steps no longer write them)
+    const TLayer& d = c->L[layer];
+    OP_HIP_CHECK(hipMemsetAsync(c->gW[layer], 0, (size_t)d.co * d.ci * d.k * d.k * 4, c->stream));
+    OP_HIP_CHECK(hipMemsetAsync(c->gb[layer], 0, (size_t)d.co * 4, c->stream));
+  }
   c->enabled[layer] = enable != 0;
   return OP_OK;
 }
@@ -833,11 +825,8 @@ int op_train_step(op_train_ctx* c, const float* x, const float* pafs_t, const fl
   TRC(tr_forward(c));
   // gradients start at zero (halos too: the input-gradient convs read them)
   OP_HIP_CHECK(hipMemsetAsync((float*)c->arena + c->grad_off, 0, c->grad_off * 4, c->stream));
-  for (int l = 0; l < kNL; ++l) {
-    const TLayer& d = c->L[l];
-    OP_HIP_CHECK(hipMemsetAsync(c->gW[l], 0, (size_t)d.co * d.ci * d.k * d.k * 4, c->stream));
-    OP_HIP_CHECK(hipMemsetAsync(c->gb[l], 0, (size_t)d.co * 4, c->stream));
-  }
+  // (no per-step gradient clearing: every enabled layer's tr_wreduce / tr_breduce assigns its whole
+  // gW / gb once per step; a disabled layer's gradients are zeroed when it is disabled)
   // compute_loss: 6 stages x (paf, heat), mean over n * C * h8 * w8 elements each
   const int64_t per = (int64_t)n * 38 * h8 * w8;
   const size_t nblocks = nb(per);
