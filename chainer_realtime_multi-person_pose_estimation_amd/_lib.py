@@ -25,7 +25,7 @@ EXPORTED = (
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
-    "op_set_conv_algo", "op_profile_classes", "op_run_staged_precise",
+    "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
@@ -84,6 +84,7 @@ def lib():
         "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
         "op_detect_precise": ([P, P, I32, I32, I64, P, P, I32, P, P, P], ctypes.c_int),
         "op_set_conv_algo": ([P, I32], ctypes.c_int),
+        "op_set_batch_invariant": ([P, I32], ctypes.c_int),
         "op_profile_classes": ([P, I32], ctypes.c_int),
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
@@ -265,6 +266,11 @@ class Context(object):
     def set_conv_algo(self, algo):
         """Kernel family of the bf16x3 convolutions (include/openpose_hip.h: op_set_conv_algo)."""
         check(lib().op_set_conv_algo(self.h, int(algo)), "op_set_conv_algo")
+
+    def set_batch_invariant(self, enable=True):
+        """One accumulation order for every batch size (include/openpose_hip.h: op_set_batch_invariant);
+        off by default: lone frames split their 7x7 input channels over workgroups (~2x lower latency)."""
+        check(lib().op_set_batch_invariant(self.h, int(bool(enable))), "op_set_batch_invariant")
 
     def detect_precise(self, img, cap=2048, return_maps=False):
         """detect_precise (pose_detector.py:433-482): (poses, scores, res[, pafs (38,h,w), heatmaps (19,h,w)])."""
@@ -526,8 +532,8 @@ class CpmContext(object):
         return self._keypoints(kp, found)
 
     def detect_batch(self, crops, thresh, flip_maps=None):
-        """``detect`` over a list of BGR crops (any sizes) in one batched forward; the same results
-        as one ``detect`` call per crop."""
+        """``detect`` over a list of BGR crops (any sizes) in one batched forward; the keypoints of
+        one ``detect`` call per crop (confidences up to f32 re-association)."""
         imgs = [np.ascontiguousarray(c, np.uint8) for c in crops]
         for img in imgs:
             if img.ndim != 3 or img.shape[2] != 3:

@@ -24,6 +24,8 @@
 //  * Workgroup -> XCD: blocks are dealt to XCDs round-robin, so block b is remapped to make every
 //    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
 //  * MFMA: v_mfma_f32_32x32x16_bf16, products hi*hi + hi*lo + lo*hi into one f32 accumulator.
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <vector>
 
@@ -50,6 +52,8 @@ struct BigTiling {
   int32_t fa_tiles;          // > 0 (conv_m16): raster tiles aligned to frames, fa_tiles per frame
   int32_t per_xcd;           // > 0: pixel-major XCD order (conv_m16k): XCD x runs pixel tiles
                              // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
+  int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
+  float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
 };
 
 template <int N>
@@ -241,7 +245,11 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     wsrc[i] = (const char*)g.w + (j / CH) * wplane + ((int64_t)co0 + 64 * (j % CH) + lane) * 16;
     wdst[i] = (j / CH) * PLANE_W + (j % CH) * 1024;
   }
-  const int n_it = s.c16 * KSQ;
+  // split-K (tl.ksplit > 1, non-PF only): this workgroup runs input chunks [cb0, cb1)
+  const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
+  const int split = nsplit > 1 ? (int)blockIdx.y : 0;
+  const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
+  const int n_it = cb1 * KSQ;
   auto stage_w = [&](int it) {
     char* dst = lds + (it % RING) * SLOT_W;  // slot of the unclamped step
     if (it >= n_it) it = n_it - 1;           // trailing copies: never read
@@ -619,7 +627,11 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int64_t wstep = 4 * wplane;
   const char* const wsrc = (const char*)g.w + (wave / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
   const int wdst = (wave / 2) * PLANE_W + (wave % 2) * 1024;
-  const int n_it = s.c16 * KSQ;
+  // split-K (tl.ksplit > 1, non-PF only): this workgroup runs input chunks [cb0, cb1)
+  const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
+  const int split = nsplit > 1 ? (int)blockIdx.y : 0;
+  const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
+  const int n_it = cb1 * KSQ;
   auto stage_w = [&](int it) {
     char* dst = lds + (it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
@@ -647,8 +659,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  stage_w(0);
-  stage_w(1);
+  stage_w(cb0 * KSQ);
+  stage_w(cb0 * KSQ + 1);
   const char* const bplane = halo + (2 * khalf) * hplane;             // hi plane; lo at + hplane
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
   const int h_plane = wave & 3, h_i0 = wave >> 2;
@@ -756,8 +768,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       }
     }
   } else {
-  int it = 0;
-  for (int c = 0; c < s.c16; ++c) {
+  int it = cb0 * KSQ;
+  for (int c = cb0; c < cb1; ++c) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #ifdef M16_SKIP_RELOAD  // timing experiment only (wrong results): halo loaded for chunk 0 only
@@ -839,6 +851,21 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
   wait_vmcnt<0>();
 
+  if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
+    const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
+    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      const int P = P0 + (pg * NPX + pb) * 16 + l16;
+      if (P > P1) continue;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+        if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
+      }
+    }
+    return;
+  }
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
 #pragma unroll
@@ -872,6 +899,59 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       if (o32) *(floatx4*)(o32 + co) = v;
     }
   }
+}
+
+// Per-stream split-K workspace (grown on demand, never freed: a captured hipGraph may keep using
+// an older buffer).  nullptr while the stream is capturing and the buffer is too small.
+static float* splitk_ws(hipStream_t st, size_t floats) {
+  static std::mutex mu;
+  static std::map<hipStream_t, std::pair<float*, size_t>> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = bufs[st];
+  if (e.second >= floats) return e.first;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  float* p = nullptr;
+  if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
+  e = {p, floats};
+  return p;
+}
+
+// Split-K epilogue of conv_m16_bf16x3: out = act(sum over splits (fixed order) + bias), stored
+// like the kernel's own epilogue (split hi/lo planes + optional dense f32).  Thread = 4 channels.
+__global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
+                                                              BigTiling tl) {
+  const int grp = blockIdx.y;
+  const SplitConvGroup g = grp == 0 ? g0 : g1;
+  const int q = g.cop / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)tl.total * q) return;
+  const int P = (int)(i / q), co = (int)(i - (int64_t)P * q) * 4;
+  if (co >= g.cout_store) return;
+  const int wsc = max(g0.cop, g1.cop);
+  floatx4 v = *(const floatx4*)(g.bias + co);
+  for (int sp = 0; sp < tl.ksplit; ++sp) {
+    const floatx4 a = *(const floatx4*)(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += a[e];
+  }
+  const int f = P / tl.hw, pp = P - f * tl.hw;
+  const int y = pp / s.w, x = pp - y * s.w;
+  const int wp_out = s.w + 2 * s.pout;
+  char* d = (char*)g.out + ((int64_t)(f * (s.h + 2 * s.pout) + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4 +
+            (co >> 3) * 32 + (co & 7) * 2;
+  u16x4g vh, vl;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (s.relu) v[e] = v[e] > 0.0f ? v[e] : 0.0f;
+    const __bf16 h16 = (__bf16)v[e];
+    const __bf16 l16v = (__bf16)(v[e] - (float)h16);
+    vh[e] = __builtin_bit_cast(unsigned short, h16);
+    vl[e] = __builtin_bit_cast(unsigned short, l16v);
+  }
+  *(u16x4g*)d = vh;
+  *(u16x4g*)(d + 16) = vl;
+  if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
 }
 
 // ---- 3x3 on v_mfma_f32_16x16x32_bf16 with K = 32 input channels (default 3x3 kernel) ----
@@ -1439,6 +1519,30 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       *taken = 1;
       static bool attr = false;
       static const bool pf = getenv("OP_M16_PF") && atoi(getenv("OP_M16_PF")) != 0;
+      // Split-K for launches that still leave most CUs idle (one frame, one crop): the input
+      // chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce), since a
+      // workgroup's time is mostly its per-chunk, per-tap-pair work, not its pixel count
+      static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
+      const int wgs = tl.xpu ? 8 * ((tl.per_unit + tl.xpu - 1) / tl.xpu) : tl.units * tl.per_unit;
+      tl.ksplit = 1;
+      tl.ws = nullptr;
+      if (s.splitk && !(pf && npx == 10)) {
+        int S = 1;
+        if (ks_force > 0) S = s.c16 % ks_force == 0 ? ks_force : 1;
+        else
+          for (int cand : {8, 4, 2})
+            if (s.c16 % cand == 0 && wgs * cand <= 256) {
+              S = cand;
+              break;
+            }
+        if (S > 1) {
+          float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
+          if (ws) {
+            tl.ksplit = S;
+            tl.ws = ws;
+          }
+        }
+      }
       if (!attr) {
         const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 10, true>,
                              (const void*)conv_m16_bf16x3<7, 8>,  (const void*)conv_m16_bf16x3<7, 6>,
@@ -1452,18 +1556,25 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+      const dim3 grid(blocks, (unsigned)tl.ksplit);
       switch (npx) {
-        case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 5: hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 4: hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 3: hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 2: hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 5: hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 4: hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 3: hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 2: hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
         default:
           if (pf)
-            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl);
+            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
           else
-            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), dim3(blocks), dim3(512), lds, st, s, g[0], g1, tl);
+            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+      }
+      if (tl.ksplit > 1) {
+        OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
+        const int64_t items = (int64_t)tl.total * (cop_max / 4);
+        hipLaunchKernelGGL(conv_m16_splitk_reduce, dim3((unsigned)((items + 255) / 256), (unsigned)s.groups), dim3(256),
+                           0, st, s, g[0], g1, tl);
       }
       OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
       OP_HIP_CHECK(hipGetLastError());

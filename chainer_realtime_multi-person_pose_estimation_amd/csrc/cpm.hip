@@ -279,6 +279,7 @@ SplitConvShape cshape(int n, const CAct& in, const CAct& out, int c16, int ks, b
   s.groups = 1;
   s.cs_out32 = 0;
   s.halo_mode = 4;
+  s.splitk = 1;
   return s;
 }
 

@@ -277,6 +277,7 @@ struct op_ctx {
   bool timed = false;
   // per-class launch profiling
   bool prof = false;
+  int splitk = 1;  // op_set_batch_invariant(0): small 7x7 launches may split K
   int prof_mask = 0xF;  // kernel classes timed while prof (op_profile_classes)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -549,7 +550,8 @@ static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_
 // Default split-path conv kernel family of new contexts (op_set_conv_algo; OP_HALO_MODE env).
 static int g_halo_mode = 4;
 
-static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups, int algo) {
+static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks, bool relu, int groups, int algo,
+                           int splitk) {
   SplitConvShape s;
   s.n = n;
   s.h = out.h;
@@ -564,6 +566,7 @@ static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks
   s.groups = groups;
   s.cs_out32 = 0;
   s.halo_mode = algo;
+  s.splitk = splitk;
   return s;
 }
 
@@ -576,7 +579,7 @@ static int conv1(op_ctx* c, const Act& in, int cin_off, const Act& out, int cout
     double fl = 0, by = 0;
     conv_work(c, out, pc, &fl, &by);
     return profiled(c, conv_class(pc.ks), fl, by, [&] {
-      return launch_conv_bf16x3(sshp(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, 1, c->conv_algo), g, c->stream);
+      return launch_conv_bf16x3(sshp(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, 1, c->conv_algo, c->splitk), g, c->stream);
     });
   }
   ConvGroup g[2];
@@ -598,7 +601,7 @@ static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& poole
     SplitConvGroup g[2];
     g[0] = sgrp(in, 0, pooled, 0, pc, ch);
     g[1] = g[0];
-    SplitConvShape sh = sshp(c->gn, in, full, pc.cin16 / 16, pc.ks, true, 1, c->conv_algo);
+    SplitConvShape sh = sshp(c->gn, in, full, pc.cin16 / 16, pc.ks, true, 1, c->conv_algo, c->splitk);
     sh.pout = pooled.pad;
     sh.cs_out = pooled.cs;
     double fl = 0, by = 0;
@@ -621,7 +624,7 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
     SplitConvGroup g[2];
     g[0] = sgrp(in, ci0, out, co0, p0, st0);
     g[1] = sgrp(in, ci1, out, co1, p1, st1);
-    SplitConvShape sh = sshp(c->gn, in, out, p0.cin16 / 16, p0.ks, relu, 2, c->conv_algo);
+    SplitConvShape sh = sshp(c->gn, in, out, p0.cin16 / 16, p0.ks, relu, 2, c->conv_algo, c->splitk);
     if (out32) {
       g[0].out32 = g[1].out32 = out32->p;
       g[0].out32_off = o32a;
@@ -1862,6 +1865,13 @@ int op_set_precision(op_ctx* c, int32_t mode) {
     return OP_ERR_INVALID;
   }
   c->split = mode == OP_PRECISION_BF16X3;
+  return OP_OK;
+}
+
+int op_set_batch_invariant(op_ctx* c, int32_t enable) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  c->splitk = enable ? 0 : 1;
   return OP_OK;
 }
 

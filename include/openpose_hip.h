@@ -107,6 +107,12 @@ int op_get_precision(op_ctx* ctx, int32_t* mode);
  * 3 co-split halo tiles (conv_halo.hip); 1 / 2 the 7x7 halo kernel with one / two halo buffers;
  * 0 the per-tap gather kernel.  Shapes a family does not take use the gather kernel. */
 int op_set_conv_algo(op_ctx* ctx, int32_t algo);
+/* Batch invariance (default off).  A launch that fills few CUs (one frame, one crop) splits the
+ * 7x7 convolutions' input channels over several workgroups and sums their f32 partials, so a
+ * frame's maps then differ from the same frame inside a larger batch by f32 re-association (~1e-5;
+ * near-threshold peaks of noisy maps can flip).  enable != 0 keeps one accumulation order for
+ * every batch size (single-frame latency ~2x). */
+int op_set_batch_invariant(op_ctx* ctx, int32_t enable);
 
 /* serializers.load_npz(weights_file, model) (pose_detector.py:26): 92 layers in op_layer_info
  * order, W as Chainer (Co, Ci, k, k) f32 and b as (Co,) f32.  Packed into the kernel layout
@@ -245,8 +251,9 @@ int op_cpm_detect(op_cpm_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int
                   int32_t flip_maps, double* keypoints, int32_t* found);
 /* op_cpm_detect over n crops of any sizes in one batched forward (demo.py:38-56's per-person face /
  * hand calls, which the reference makes one at a time): crop i = bgr[i] (h[i] x w[i] x 3 u8, row
- * stride row_stride[i]), flip_maps[i] as above (may be NULL: none).  Results are identical to n
- * op_cpm_detect calls: keypoints (n, c-1, 3) f64, found (n, c-1). */
+ * stride row_stride[i]), flip_maps[i] as above (may be NULL: none).  Results equal n op_cpm_detect
+ * calls up to f32 re-association (a lone crop's 7x7 convs split their input chunks over workgroups):
+ * keypoints (n, c-1, 3) f64, found (n, c-1). */
 int op_cpm_detect_batch(op_cpm_ctx* ctx, int32_t n, const uint8_t* const* bgr, const int32_t* h, const int32_t* w,
                         const int64_t* row_stride, float thresh, const int32_t* flip_maps, double* keypoints,
                         int32_t* found);

@@ -79,9 +79,19 @@ def test_cpm_detect_equals_oracle_composition(cpm, hw, hand_type):
     _same(got, exp)
 
 
+def _close(got, exp):
+    """Same keypoints; confidences equal up to f32 re-association (a single crop's 7x7 launches
+    split their input chunks over workgroups, a batch's do not)."""
+    assert len(got) == len(exp)
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert (g is None) == (e is None), i
+        if g is not None:
+            assert g[0] == e[0] and g[1] == e[1] and abs(float(g[2]) - float(e[2])) <= 1e-5 * max(1.0, abs(float(e[2]))), (i, g, e)
+
+
 def test_cpm_detect_batch_equals_single_calls(cpm):
     """op_cpm_detect_batch over crops of mixed sizes (and mixed left/right readouts) == one
-    op_cpm_detect per crop, bit for bit."""
+    op_cpm_detect per crop: the same keypoints, confidences up to f32 re-association."""
     arch, c, _ = cpm
     rng = np.random.default_rng(11)
     sizes = [(96, 80), (61, 75), (300, 210), (40, 33), (368, 368)]
@@ -92,7 +102,7 @@ def test_cpm_detect_batch_equals_single_calls(cpm):
         batch = c.detect_batch(crops, thr, flip_maps=flips)
         assert len(batch) == len(single)
         for g, e in zip(batch, single):
-            _same(g, e)
+            _close(g, e)
     assert c.detect_batch([], 0.1) == []
     with pytest.raises(ValueError):
         c.detect_batch([crops[0], crops[1][:1]], 0.1)  # a 1-row crop: rejected like op_cpm_detect

@@ -154,16 +154,25 @@ def test_conv_algos_agree(ctx, algo):
 
 
 def test_forward_7x7_tile_sizes_agree(ctx):
-    """The 7x7 raster kernel picks 640-, 256- or 128-px tiles by how many workgroups a launch
-    gets (batch 16 at 368x368: 256-px; one frame: 128-px); the per-pixel MFMA accumulation order
-    does not depend on the tile, so a frame's maps match between batch 16 and batch 1."""
+    """The 7x7 raster kernel picks its tile size by how many workgroups a launch gets (batch 16 at
+    368x368: 320-px tiles; one frame: 128-px tiles with the input chunks split over 4 workgroups
+    and the f32 partials summed by conv_m16_splitk_reduce); a frame's maps agree between batch
+    16 and batch 1 up to that f32 re-association."""
     rng = np.random.default_rng(16)
     x = rng.uniform(-0.5, 0.5, (16, 3, 368, 368)).astype(np.float32)
     pb, hb = ctx.forward(x)
+    ctx.set_batch_invariant(True)  # tile sizes alone do not change a pixel's accumulation order
+    try:
+        for i in (0, 15):
+            p1, h1 = ctx.forward(x[i:i + 1])
+            assert np.array_equal(pb[i], p1[0]) and np.array_equal(hb[i], h1[0])
+    finally:
+        ctx.set_batch_invariant(False)
     for i in (0, 7, 15):
         p1, h1 = ctx.forward(x[i:i + 1])
         err = max(float(np.abs(pb[i] - p1[0]).max()), float(np.abs(hb[i] - h1[0]).max()))
-        assert err <= 1e-6, (i, err)
+        mag = max(1.0, float(np.abs(pb[i]).max()), float(np.abs(hb[i]).max()))
+        assert err <= 1e-4 * mag, (i, err, mag)  # 10x inside the 1e-3 parity tolerance
 
 
 def test_forward_precisions_agree(ctx, rand_weights):
@@ -194,7 +203,12 @@ def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
 
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
 def test_staged_batch_matches_single_and_graph(ctx, prec):
+    """A staged batch (eager and hipGraph replay) gives each frame exactly the result of a
+    single-frame detect in batch-invariant mode (op_set_batch_invariant: no split-K for the lone
+    frame's 7x7 launches)."""
     ctx.set_precision(prec)
+    ctx.set_batch_invariant(True)
+
     rng = np.random.default_rng(3)
     frames = rng.integers(0, 256, (3, 300, 420, 3), dtype=np.uint8)
     single = [ctx.detect(f) for f in frames]
@@ -210,6 +224,7 @@ def test_staged_batch_matches_single_and_graph(ctx, prec):
             assert r.n_peaks == single[i][2].n_peaks and r.status == 0
             assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
     ctx.set_precision("bf16x3")
+    ctx.set_batch_invariant(False)
 
 
 def test_staged_synthetic_maps_match_reference(ctx):
