@@ -1016,7 +1016,11 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
   // weights: 16 1-KiB pieces per step; wave w copies j = 4w .. 4w+3: chunk j/8, plane (j/2)%4, half j%2
   const int64_t wplane = (int64_t)g.cop * 16;
   const int64_t wstep = 4 * wplane;  // one (chunk, tap)
-  const int n_it = (s.c16 / 2) * KSQ;
+  // split-K (tl.ksplit > 1, not with the pooled epilogue): chunk pairs [cp0, cp1) of this workgroup
+  const int nsplit = (!POOL && tl.ksplit > 1) ? tl.ksplit : 1;
+  const int split = nsplit > 1 ? (int)blockIdx.y : 0;
+  const int cp0 = split * (s.c16 / 2 / nsplit), cp1 = cp0 + s.c16 / 2 / nsplit;
+  const int n_it = cp1 * KSQ;
   auto stage_w = [&](int it) {
     char* dst = lds + (it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
@@ -1050,12 +1054,12 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  stage_w(0);
+  stage_w(cp0 * KSQ);
   const char* const bplane = halo + (csel * 4 + 2 * khalf) * hplane;          // hi plane; lo at + hplane
   const int wlane = csel * CHUNK_W + (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;
   // halo reload: 8 planes x nh pieces over 4 waves; wave w: planes w and w + 4 (chunk 0 / 1)
-  int it = 0;
-  for (int cp = 0; cp < s.c16 / 2; ++cp) {
+  int it = cp0 * KSQ;
+  for (int cp = cp0; cp < cp1; ++cp) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -1161,6 +1165,23 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
     return;
   }
 
+  if (nsplit > 1) {  // raw partials in raster order (conv_m16_splitk_reduce finishes them)
+    const int wsc = max(g0.cop, g1.cop);
+    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      const int b = pg * NPX + pb;
+      const int r = b / TCB, c = (b % TCB) * 16 + l16;
+      if (r >= rows_here || c >= cols_here) continue;
+      const int64_t P = ((int64_t)frame * s.h + y0 + r) * s.w + x0 + c;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+        if (co < g.cop) *(floatx4*)(wsg + P * wsc + co) = acc[cb][pb];
+      }
+    }
+    return;
+  }
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
 #pragma unroll
@@ -1418,13 +1439,50 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
                           : tl.xpu   ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+  // split-K when the launch fills few of the 512 workgroup slots (two per CU): one frame's
+  // 46-wide layers (12-48 workgroups); partials reduced by conv_m16_splitk_reduce
+  BigTiling t = tl;
+  t.ksplit = 1;
+  t.ws = nullptr;
+  static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
+  if (!pool && s.splitk) {
+    const int pairs = s.c16 / 2;
+    int S = 1;
+    if (ks_force > 0) S = pairs % ks_force == 0 ? ks_force : 1;
+    else
+      for (int cand : {8, 4, 2})
+        if (pairs % cand == 0 && (int)blocks * cand <= 512) {
+          S = cand;
+          break;
+        }
+    if (S > 1) {
+      int cop_max = g[0].cop;
+      if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
+      t.hw = s.h * s.w;
+      t.total = s.n * s.h * s.w;
+      float* ws = splitk_ws(st, (size_t)S * s.groups * t.total * cop_max);
+      if (ws) {
+        t.ksplit = S;
+        t.ws = ws;
+      }
+    }
+  }
+  const dim3 grid(blocks, (unsigned)t.ksplit);
   if (pool)
-    hipLaunchKernelGGL(conv_m16k_bf16x3<true>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+    hipLaunchKernelGGL(conv_m16k_bf16x3<true>, grid, dim3(256), lds, st, s, g[0], g1, t);
   else if (tl.tc == 48)
-    hipLaunchKernelGGL((conv_m16k_bf16x3<false, 3, 6>), dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+    hipLaunchKernelGGL((conv_m16k_bf16x3<false, 3, 6>), grid, dim3(256), lds, st, s, g[0], g1, t);
   else
-    hipLaunchKernelGGL(conv_m16k_bf16x3<false>, dim3(blocks), dim3(256), lds, st, s, g[0], g1, tl);
+    hipLaunchKernelGGL(conv_m16k_bf16x3<false>, grid, dim3(256), lds, st, s, g[0], g1, t);
   OP_AFTER_LAUNCH("conv_m16k_bf16x3", st);
+  if (t.ksplit > 1) {
+    int cop_max = g[0].cop;
+    if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
+    const int64_t items = (int64_t)t.total * (cop_max / 4);
+    hipLaunchKernelGGL(conv_m16_splitk_reduce, dim3((unsigned)((items + 255) / 256), (unsigned)s.groups), dim3(256), 0,
+                       st, s, g[0], g1, t);
+    OP_AFTER_LAUNCH("conv_m16_splitk_reduce", st);
+  }
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }

@@ -155,19 +155,21 @@ def test_conv_algos_agree(ctx, algo):
 
 def test_forward_7x7_tile_sizes_agree(ctx):
     """The 7x7 raster kernel picks its tile size by how many workgroups a launch gets (batch 16 at
-    368x368: 320-px tiles; one frame: 128-px tiles with the input chunks split over 4 workgroups
-    and the f32 partials summed by conv_m16_splitk_reduce); a frame's maps agree between batch
-    16 and batch 1 up to that f32 re-association."""
+    368x368: 320-px tiles; one frame: 128-px tiles), which leaves a pixel's accumulation order
+    alone (exact in batch-invariant mode); by default launches that fill few CUs also split their
+    input chunks over workgroups (7x7 and 3x3, f32 partials summed by conv_m16_splitk_reduce), so
+    a frame's maps agree between batch 16 and batch 1 up to that f32 re-association."""
     rng = np.random.default_rng(16)
     x = rng.uniform(-0.5, 0.5, (16, 3, 368, 368)).astype(np.float32)
-    pb, hb = ctx.forward(x)
     ctx.set_batch_invariant(True)  # tile sizes alone do not change a pixel's accumulation order
     try:
+        pi, hi = ctx.forward(x)
         for i in (0, 15):
             p1, h1 = ctx.forward(x[i:i + 1])
-            assert np.array_equal(pb[i], p1[0]) and np.array_equal(hb[i], h1[0])
+            assert np.array_equal(pi[i], p1[0]) and np.array_equal(hi[i], h1[0])
     finally:
         ctx.set_batch_invariant(False)
+    pb, hb = ctx.forward(x)  # default: split-K where a launch fills few CUs
     for i in (0, 7, 15):
         p1, h1 = ctx.forward(x[i:i + 1])
         err = max(float(np.abs(pb[i] - p1[0]).max()), float(np.abs(hb[i] - h1[0]).max()))

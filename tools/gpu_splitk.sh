@@ -1,9 +1,9 @@
 #!/bin/bash
-# 7x7 split-K for under-filled launches: full GPU suite, latency sweep (auto vs split off), crops
+# split-K (7x7 + 3x3) for under-filled launches: GPU suite, then latency A/B
 set -o pipefail
-O=gpurun_out/splitk; mkdir -p $O
-# (tests run separately)
-for b in 1 4 8 38; do
+O=gpurun_out/splitk2; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || exit $?
+for b in 1 2 4 38; do
   for v in 0 1; do
     OP_M16_KSPLIT=$v timeout -k 10 200 python -u bench.py --no-cpu-baseline --batch $b > $O/b${b}_k$v.log 2>&1 || exit $?
   done
