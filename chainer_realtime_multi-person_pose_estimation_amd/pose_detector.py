@@ -26,10 +26,13 @@ class PoseDetector(object):
     precise: multi-scale inference (pose_detector.py:433-482).
     precision: 'bf16x3' (default; 3xBF16-split products with f32 accumulation, |err| ~3e-5 on the
                maps) or 'fp32' (exact f32 products on the f32 matrix cores).
+    batch_invariant: keep one accumulation order for every batch size (by default a lone frame's
+               convolutions split their input channels over workgroups: ~2x lower latency, f32
+               re-association ~1e-5 against the same frame in a batch).
     """
 
     def __init__(self, arch=None, weights_file=None, model=None, device=-1, precise=False, max_batch=1,
-                 precision="bf16x3"):
+                 precision="bf16x3", batch_invariant=False):
         self.arch = arch
         self.precise = precise
         if model is None and arch not in (None, "posenet"):
@@ -39,6 +42,8 @@ class PoseDetector(object):
         limits.max_batch = int(max_batch)
         self._ctx = _lib.Context(self.device, _lib.params_from_dict(params), limits)
         self._ctx.set_precision(precision)
+        if batch_invariant:  # one accumulation order for every batch size (op_set_batch_invariant)
+            self._ctx.set_batch_invariant(True)
         if model is not None:
             w = model
         elif weights_file:
