@@ -24,6 +24,7 @@
 //  * Workgroup -> XCD: blocks are dealt to XCDs round-robin, so block b is remapped to make every
 //    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
 //  * MFMA: v_mfma_f32_32x32x16_bf16, products hi*hi + hi*lo + lo*hi into one f32 accumulator.
+#include <array>
 #include <map>
 #include <mutex>
 #include <cstdlib>
@@ -1545,32 +1546,47 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     if (s.halo_mode != 9 && s.halo_mode != 10 && s.halo_mode != 11 &&
         raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
-      // Tile size for launches that leave CUs idle.  A workgroup's time grows as ~(2 + NPX) (fixed
-      // halo / weight-ring / barrier work plus NPX 16-px blocks per wave; measured 0.17 / 0.25 /
-      // 0.50 ms for NPX 2 / 4 / 10), one workgroup per CU, so a launch costs
-      // rounds x (2 + NPX) with rounds = workgroups per XCD / 32 CUs, rounded up.  640-px tiles
-      // (NPX 10) stay whenever they come close to filling the chip (the 38-frame batch: 252);
-      // otherwise the cheapest of NPX 8, 6, 5, 4, 3, 2 (one crop: 2; 16 frames: 5 -> 212
-      // workgroups in one round instead of 106 at 2.4x the work each).
+      // Tile size per launch shape.  A workgroup's time grows as ~(2 + NPX) (fixed halo /
+      // weight-ring / barrier work plus NPX 16-px blocks per wave; measured 0.17 / 0.25 / 0.50 ms
+      // for NPX 2 / 4 / 10), one workgroup per CU, so a launch costs rounds x (2 + NPX) with
+      // rounds = workgroups per XCD / 32 CUs, rounded up.  640-px tiles (NPX 10) stay unless a
+      // smaller tile costs less (the 38-frame batch: 252 workgroups, one round, kept); the
+      // candidates are NPX 8, 6, 5, 4, 3, 2 (one crop: 2; 16 frames: 5 -> 212
+      // workgroups in one round instead of 106 at 2.4x the work each; 40-57 frames: 8, two
+      // rounds of 512-px tiles instead of two of 640).
       static const int force = getenv("OP_M16_NPX") ? atoi(getenv("OP_M16_NPX")) : 0;  // A/B aid
       auto rounds = [](const BigTiling& t) -> int {
         return t.xpu ? ((t.per_unit + t.xpu - 1) / t.xpu + 31) / 32 : (t.units * t.per_unit + 255) / 256;
       };
+      // every launch shape is evaluated once (the tilings loop over tiles) and cached
+      static std::mutex sel_mu;
+      static std::map<std::array<int, 5>, std::pair<int, BigTiling>> sel_cache;
+      const std::array<int, 5> key{s.n, s.h, s.w, s.groups, cop_max};
       int npx = 10;
-      if (force != 10 && (force || tl.units * tl.per_unit < 230)) {
-        int best = rounds(tl) * (2 + 10);
-        for (int cand : {8, 6, 5, 4, 3, 2}) {
-          if (force && cand != force) continue;
-          BigConfig k{7, 1, 8, 128, 1, 0, 1};
-          k.cap_px = 64 * cand;
-          BigTiling tc{};
-          if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
-          const int cost = rounds(tc) * (2 + cand);
-          if (force || cost < best) {
-            best = cost;
-            npx = cand;
-            tl = tc;
+      {
+        std::lock_guard<std::mutex> lk(sel_mu);
+        auto it = sel_cache.find(key);
+        if (it != sel_cache.end()) {
+          npx = it->second.first;
+          tl = it->second.second;
+        } else {
+          if (force != 10) {
+            int best = rounds(tl) * (2 + 10);
+            for (int cand : {8, 6, 5, 4, 3, 2}) {
+              if (force && cand != force) continue;
+              BigConfig k{7, 1, 8, 128, 1, 0, 1};
+              k.cap_px = 64 * cand;
+              BigTiling tc{};
+              if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
+              const int cost = rounds(tc) * (2 + cand);
+              if (force || cost < best) {
+                best = cost;
+                npx = cand;
+                tl = tc;
+              }
+            }
           }
+          sel_cache[key] = {npx, tl};
         }
       }
       if (plain_order) tl.xpu = 0;
