@@ -64,6 +64,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
 #endif
 }
 
+// global -> LDS copy with an explicit cache-policy operand (timing experiments: 2 = nt)
+template <int AUX>
+__device__ __forceinline__ void glds16a(const void* gsrc, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, AUX);
+}
+
 // ---- launch helpers implemented in the .hip files ----
 struct ConvGroup {
   const float* in;    // padded NHWC input, already offset by the group's first input channel

@@ -39,6 +39,14 @@ typedef unsigned short u16x4g __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR_G(p) ((__attribute__((address_space(3))) void*)(p))
 
+// cache policy of the conv_m16 / conv_m16k halo loads (timing experiments; 0 = default)
+#ifndef M16_HALO_AUX
+#define M16_HALO_AUX 0
+#endif
+#ifndef M16K_HALO_AUX
+#define M16K_HALO_AUX 0
+#endif
+
 struct BigTiling {
   int32_t tr, tc;            // tile rows x cols
   int32_t tiles_y, tiles_x;  // tiles per frame
@@ -785,7 +793,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(hc - R + s.pin, wp_in - 1);
-        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
+        glds16a<M16_HALO_AUX>((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 2 * 1024;
         hc += 2 * 64;
         while (hc >= tl.pitch) {
@@ -1070,7 +1078,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
       int hr = lane / tl.pitch, hc = lane - (lane / tl.pitch) * tl.pitch;
       for (int i = 0; i < tl.nh; ++i) {
         const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-        glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
+        glds16a<M16K_HALO_AUX>((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 1024;
         hc += 64;
         while (hc >= tl.pitch) {
