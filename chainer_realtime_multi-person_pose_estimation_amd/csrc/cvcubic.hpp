@@ -15,9 +15,11 @@ struct CubicTap {
   float c[4];  // interpolateCubic coefficients
 };
 
-__device__ __forceinline__ CubicTap cv_cubic_tap(int d, int dsize, int ssize) {
-  const double inv = __ddiv_rn((double)dsize, (double)ssize);
-  const double scale = __ddiv_rn(1.0, inv);
+// scale = 1 / (dsize / ssize) in double (OpenCV's inv_scale_x / scale_x); host launchers pass it
+// precomputed (IEEE division on the host rounds the same), sparing two f64 divisions per thread
+__host__ __device__ inline double cv_cubic_scale(int dsize, int ssize) { return 1.0 / ((double)dsize / (double)ssize); }
+
+__device__ __forceinline__ CubicTap cv_cubic_tap_s(int d, double scale) {
   float f = __double2float_rn(__dsub_rn(__dmul_rn(__dadd_rn((double)d, 0.5), scale), 0.5));
   const int si = (int)floorf(f);
   f = __fsub_rn(f, (float)si);
@@ -33,6 +35,11 @@ __device__ __forceinline__ CubicTap cv_cubic_tap(int d, int dsize, int ssize) {
   t.c[2] = __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(__fmul_rn(1.25f, y), 2.25f), y), y), 1.0f);
   t.c[3] = __fsub_rn(__fsub_rn(__fsub_rn(1.0f, t.c[0]), t.c[1]), t.c[2]);
   return t;
+}
+
+__device__ __forceinline__ CubicTap cv_cubic_tap(int d, int dsize, int ssize) {
+  const double inv = __ddiv_rn((double)dsize, (double)ssize);
+  return cv_cubic_tap_s(d, __ddiv_rn(1.0, inv));
 }
 
 __device__ __forceinline__ int cv_cubic_fix(float c) {  // saturate_cast<short>(c * 2048)

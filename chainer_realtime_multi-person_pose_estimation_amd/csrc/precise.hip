@@ -78,7 +78,7 @@ int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, 
 //   (the running sum over scales of pose_detector.py:463/467 and its mean at :469-470).
 __global__ __launch_bounds__(256) void resize_cubic_f32(const float* __restrict__ src, int64_t sstride, int pstride,
                                                         int sh, int sw, int cn, float* __restrict__ dst, int dh, int dw,
-                                                        int mode, float div) {
+                                                        int mode, float div, double scx, double scy) {
   const int64_t total = (int64_t)cn * dh * dw;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -92,8 +92,8 @@ __global__ __launch_bounds__(256) void resize_cubic_f32(const float* __restrict_
     y = (int)((i / dw) % dh);
     c = (int)(i / ((int64_t)dw * dh));
   }
-  const CubicTap tx = cv_cubic_tap(x, dw, sw);
-  const CubicTap ty = cv_cubic_tap(y, dh, sh);
+  const CubicTap tx = cv_cubic_tap_s(x, scx);
+  const CubicTap ty = cv_cubic_tap_s(y, scy);
   const float v = cv_cubic_f32(src, sstride, pstride, sh, sw, c, tx, ty, x * cn + c, dw * cn / 4 * 4);
   if (mode == 0) {
     dst[i] = v;
@@ -110,7 +110,7 @@ int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, 
                             float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st) {
   const int64_t total = (int64_t)cn * dh * dw;
   hipLaunchKernelGGL(resize_cubic_f32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, sstride, pstride,
-                     sh, sw, cn, dst, dh, dw, mode, div);
+                     sh, sw, cn, dst, dh, dw, mode, div, cv_cubic_scale(dw, sw), cv_cubic_scale(dh, sh));
   OP_AFTER_LAUNCH("resize_cubic_f32", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
@@ -124,12 +124,12 @@ int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, 
 __global__ __launch_bounds__(256) void resize_cubic_f32_planar(const float* __restrict__ src, int64_t cstride,
                                                                int64_t sstride, int sh, int sw, int cn,
                                                                float* __restrict__ dst, int dh, int dw, int mode,
-                                                               float div) {
+                                                               float div, double scx, double scy) {
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y = blockIdx.y, c = blockIdx.z;
   if (x >= dw) return;
-  const CubicTap tx = cv_cubic_tap(x, dw, sw);
-  const CubicTap ty = cv_cubic_tap(y, dh, sh);
+  const CubicTap tx = cv_cubic_tap_s(x, scx);
+  const CubicTap ty = cv_cubic_tap_s(y, scy);
   const float v = cv_cubic_f32(src, sstride, 1, sh, sw, c, tx, ty, x * cn + c, dw * cn / 4 * 4, cstride);
   const int64_t i = ((int64_t)c * dh + y) * dw + x;
   if (mode == 1) {
@@ -149,7 +149,8 @@ int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t ss
     return OP_ERR_INVALID;
   }
   hipLaunchKernelGGL(resize_cubic_f32_planar, dim3((unsigned)((dw + 255) / 256), (unsigned)dh, (unsigned)cn),
-                     dim3(256), 0, st, src, cstride, sstride, sh, sw, cn, dst, dh, dw, mode, div);
+                     dim3(256), 0, st, src, cstride, sstride, sh, sw, cn, dst, dh, dw, mode, div, cv_cubic_scale(dw, sw),
+                     cv_cubic_scale(dh, sh));
   OP_AFTER_LAUNCH("resize_cubic_f32_planar", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
