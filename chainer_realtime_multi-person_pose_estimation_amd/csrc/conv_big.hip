@@ -847,12 +847,18 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         bl[cur ^ 1] = bl[cur];
 #endif
         __builtin_amdgcn_sched_barrier(0);
+#ifdef M16_SETPRIO  // timing experiment: MFMA clusters at raised wave priority
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
         }
+#ifdef M16_SETPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
       }
       it += two ? 2 : 1;
     }
