@@ -20,7 +20,7 @@ N_JOINTS, N_LIMBS, N_PAF, N_HEAT, N_LAYERS = 18, 19, 38, 19, 92
 # Every symbol include/openpose_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "op_last_error", "op_default_params", "op_default_limits", "op_layer_info", "op_create", "op_destroy",
-    "op_set_weights", "op_detect", "op_preprocess", "op_forward", "op_resize_images", "op_compute_peaks",
+    "op_set_weights", "op_detect", "op_preprocess", "op_forward", "op_forward_stages", "op_resize_images", "op_compute_peaks",
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
@@ -89,6 +89,7 @@ def lib():
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
         "op_forward": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
+        "op_forward_stages": ([P, P, I32, I32, I32, P, P], ctypes.c_int),
         "op_resize_images": ([P, P, I32, I32, I32, I32, I32, P], ctypes.c_int),
         "op_compute_peaks": ([P, P, I32, I32, I32, P, I64, P], ctypes.c_int),
         "op_compute_connections": ([P, P, I32, I32, P, I64, D, P, I64, P], ctypes.c_int),
@@ -323,6 +324,17 @@ class Context(object):
         paf = np.empty((n, N_PAF, h // 8, w // 8), np.float32)
         heat = np.empty((n, N_HEAT, h // 8, w // 8), np.float32)
         check(lib().op_forward(self.h, ptr(x), n, h, w, ptr(paf), ptr(heat)), "op_forward")
+        return paf, heat
+
+    def forward_stages(self, x):
+        """All six stages: pafs (6, n, 38, h/8, w/8), heatmaps (6, n, 19, h/8, w/8)."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n, c, h, w = x.shape
+        if c != 3:
+            raise ValueError("expected (n, 3, h, w)")
+        paf = np.empty((6, n, N_PAF, h // 8, w // 8), np.float32)
+        heat = np.empty((6, n, N_HEAT, h // 8, w // 8), np.float32)
+        check(lib().op_forward_stages(self.h, ptr(x), n, h, w, ptr(paf), ptr(heat)), "op_forward_stages")
         return paf, heat
 
     def resize_images(self, x, oh, ow):

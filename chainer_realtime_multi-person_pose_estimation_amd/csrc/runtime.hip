@@ -702,9 +702,19 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
 }
 
 // frames != nullptr (split path): conv1_1 reads the uint8 frames directly (fused input kernel).
+// stages != nullptr: every stage's (paf, heat) is also extracted to stages = paf [6][n][38][lh][lw]
+// followed by heat [6][n][19][lh][lw] (op_forward_stages; the reference's pafs / heatmaps lists).
 static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame_bytes = 0, int64_t row_stride = 0,
-                       int sh = 0, int sw = 0) {
+                       int sh = 0, int sw = 0, float* stages = nullptr) {
   Act* B = c->buf;
+  const size_t stage_px = (size_t)c->gn * (c->gh / 8) * (c->gw / 8);
+  auto dump_stage = [&](int s) -> int {
+    if (!stages) return OP_OK;
+    float* paf = stages + (size_t)s * 38 * stage_px;
+    float* heat = stages + (size_t)6 * 38 * stage_px + (size_t)s * 19 * stage_px;
+    if (c->split) return launch_extract_maps32(B[B_MAP32].p, 64, 40, c->gn, c->gh / 8, c->gw / 8, paf, heat, c->stream);
+    return launch_extract_maps(B[B_CAT].p, c->gn, c->gh / 8, c->gw / 8, paf, heat, c->stream);
+  };
   static const bool c11_mfma = getenv("OP_CONV11_MFMA") != nullptr;  // debugging aid: the MFMA conv1_1
   // conv1_1 + conv1_2 + pool in one launch (conv1_pair.hip); OP_CONV1_FUSED=0: the two-kernel path
   static const bool c1_fused = !(getenv("OP_CONV1_FUSED") && atoi(getenv("OP_CONV1_FUSED")) == 0);
@@ -748,13 +758,15 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   RC(conv2(c, B[B_BRA], 0, 128, B[B_BRB], 0, 128, c->s1_g[0][0], c->s1_g[1][0], 128, 128, true));
   RC(conv2(c, B[B_BRB], 0, 128, B[B_BRA], 0, 128, c->s1_g[0][1], c->s1_g[1][1], 128, 128, true));
   {
+    const Act* m32 = (c->split && stages) ? &B[B_MAP32] : nullptr;
     const PackedConv a[2] = {c->s1_g[0][2], c->s1_g[1][2]}, b[2] = {c->s1_last[0], c->s1_last[1]};
-    const int h = head2(c, B[B_BRA], 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, nullptr, 0, 0);
+    const int h = head2(c, B[B_BRA], 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
     if (h > 0) return h;
     if (h < 0) {
       RC(conv2(c, B[B_BRA], 0, 128, s1, 0, 512, c->s1_g[0][2], c->s1_g[1][2], 512, 512, true));
-      RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false));
+      RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false, m32, 0, 40));
     }
+    RC(dump_stage(0));
   }
   // stages 2-6 (CocoPoseNet.py:167-260)
   Act s6 = B[B_S1];
@@ -768,7 +780,7 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
       std::swap(src, dst);
     }
     // the last stage also leaves a dense f32 copy (paf at 0, heat at 40) for the post-process
-    const Act* m32 = (c->split && st == 4) ? &B[B_MAP32] : nullptr;
+    const Act* m32 = (c->split && (st == 4 || stages)) ? &B[B_MAP32] : nullptr;
     const PackedConv a[2] = {c->st_g[st][0][4], c->st_g[st][1][4]}, b[2] = {c->st_last[st][0], c->st_last[st][1]};
     const int h = head2(c, *src, 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
     if (h > 0) return h;
@@ -777,6 +789,7 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
       RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false, m32, 0,
                40));
     }
+    RC(dump_stage(st + 1));
   }
   return OP_OK;
 }
@@ -1130,6 +1143,32 @@ int op_preprocess(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t r
                                 c->stream));
   RC(launch_preprocess_planar(din, (int64_t)w * 3, h, w, out_h, out_w, dout, c->stream));
   OP_HIP_CHECK(hipMemcpyAsync(x_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return OP_OK;
+}
+
+int op_forward_stages(op_ctx* c, const float* x, int32_t n, int32_t h, int32_t w, float* pafs, float* heatmaps) {
+  using namespace op;
+  RC(check_ctx(c, true));
+  if (!x || !pafs || !heatmaps) {
+    set_error("op_forward_stages: null pointer");
+    return OP_ERR_INVALID;
+  }
+  RC(ensure_geometry(c, n, h, w));
+  const size_t xin = (size_t)n * 3 * h * w * 4;
+  const size_t px = (size_t)n * (h / 8) * (w / 8);
+  const size_t outb = 6 * 57 * px * 4;
+  RC(ensure_scratch(c, xin + 256 + outb));
+  float* dx = c->d_scratch;
+  float* dst = (float*)((char*)c->d_scratch + (xin + 255) / 256 * 256);
+  OP_HIP_CHECK(hipMemcpyAsync(dx, x, xin, hipMemcpyHostToDevice, c->stream));
+  if (c->split)
+    RC(launch_nchw_to_split16(dx, c->buf[B_X0].p, n, h, w, c->stream));
+  else
+    RC(launch_nchw_to_nhwc8(dx, c->buf[B_X0].p, n, h, w, c->stream));
+  RC(run_forward(c, nullptr, 0, 0, 0, 0, dst));
+  OP_HIP_CHECK(hipMemcpyAsync(pafs, dst, 6 * 38 * px * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(heatmaps, dst + 6 * 38 * px, 6 * 19 * px * 4, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   return OP_OK;
 }

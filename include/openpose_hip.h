@@ -152,6 +152,11 @@ int op_preprocess(op_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int64_t
  * pafs (n, 38, h/8, w/8) and heatmaps (n, 19, h/8, w/8).  h, w multiples of 8. */
 int op_forward(op_ctx* ctx, const float* x, int32_t n, int32_t h, int32_t w, float* pafs, float* heatmaps);
 
+/* As op_forward, but every stage's outputs: the (pafs, heatmaps) lists CocoPoseNet.__call__ returns
+ * (models/CocoPoseNet.py:164-165, 180-181, ..., 262).  pafs (6, n, 38, h/8, w/8), heatmaps
+ * (6, n, 19, h/8, w/8); stage s at index s-1. */
+int op_forward_stages(op_ctx* ctx, const float* x, int32_t n, int32_t h, int32_t w, float* pafs, float* heatmaps);
+
 /* F.resize_images (pose_detector.py:501-502; Chainer <= 6 align-corners bilinear): (c,h,w) -> (c,oh,ow). */
 int op_resize_images(op_ctx* ctx, const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y);
 
