@@ -27,7 +27,7 @@ EXPORTED = (
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
-    "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch",
+    "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
     "op_train_enable_layer", "op_train_step",
 )
@@ -120,6 +120,7 @@ def lib():
         "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect_batch": ([P, I32, P, P, P, P, ctypes.c_float, P, P, P], ctypes.c_int),
+        "op_cpm_set_batch_invariant": ([P, I32], ctypes.c_int),
         "op_train_create": ([I32, I32, I32, I32, P], ctypes.c_int),
         "op_train_destroy": ([P], ctypes.c_int),
         "op_train_set_weights": ([P, P, P], ctypes.c_int),
@@ -472,6 +473,15 @@ def cpm_layer_table(arch):
     return out
 
 
+def _row_strided_u8(img):
+    """A uint8 H x W x 3 view whose pixels are packed within each row (rows may be strided, e.g. a
+    crop view into a larger image: the device upload packs them); anything else is copied."""
+    a = np.asarray(img)
+    if a.dtype != np.uint8 or a.ndim != 3 or a.strides[2] != 1 or a.strides[1] != 3 or a.strides[0] < a.shape[1] * 3:
+        a = np.ascontiguousarray(a, np.uint8)
+    return a
+
+
 class CpmContext(object):
     """Owns one op_cpm_ctx: a FaceNet or HandNet replica on one device (face/hand detectors)."""
 
@@ -484,6 +494,11 @@ class CpmContext(object):
         h = ctypes.c_void_p()
         check(lib().op_cpm_create(ARCH[arch], int(device), ctypes.byref(h)), "op_cpm_create")
         self.h = h
+
+    def set_batch_invariant(self, enable=True):
+        """No split-K on small launches: a crop's keypoints and confidences do not depend on the
+        other crops of its batch (include/openpose_hip.h: op_cpm_set_batch_invariant)."""
+        check(lib().op_cpm_set_batch_invariant(self.h, int(bool(enable))), "op_cpm_set_batch_invariant")
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
@@ -533,20 +548,21 @@ class CpmContext(object):
         return self._keypoints(kp, found)
 
     def detect(self, bgr, thresh, flip_maps=False):
-        img = np.ascontiguousarray(bgr, np.uint8)
+        img = _row_strided_u8(bgr)
         if img.ndim != 3 or img.shape[2] != 3:
             raise ValueError("expected an H x W x 3 uint8 BGR image")
         h, w = img.shape[:2]
         kp = np.zeros((self.n_maps - 1, 3), np.float64)
         found = np.zeros(self.n_maps - 1, np.int32)
-        check(lib().op_cpm_detect(self.h, ptr(img), h, w, w * 3, float(thresh), int(bool(flip_maps)), ptr(kp),
+        check(lib().op_cpm_detect(self.h, ctypes.c_void_p(img.ctypes.data), h, w, img.strides[0], float(thresh),
+                                  int(bool(flip_maps)), ptr(kp),
                                   ptr(found)), "op_cpm_detect")
         return self._keypoints(kp, found)
 
     def detect_batch(self, crops, thresh, flip_maps=None):
         """``detect`` over a list of BGR crops (any sizes) in one batched forward; the keypoints of
         one ``detect`` call per crop (confidences up to f32 re-association)."""
-        imgs = [np.ascontiguousarray(c, np.uint8) for c in crops]
+        imgs = [_row_strided_u8(c) for c in crops]
         for img in imgs:
             if img.ndim != 3 or img.shape[2] != 3:
                 raise ValueError("expected H x W x 3 uint8 BGR crops")
@@ -556,7 +572,7 @@ class CpmContext(object):
         ptrs = (ctypes.c_void_p * n)(*[img.ctypes.data for img in imgs])
         hs = np.array([img.shape[0] for img in imgs], np.int32)
         ws = np.array([img.shape[1] for img in imgs], np.int32)
-        rs = np.array([img.shape[1] * 3 for img in imgs], np.int64)
+        rs = np.array([img.strides[0] for img in imgs], np.int64)
         fl = np.array([int(bool(f)) for f in (flip_maps or [False] * n)], np.int32)
         if len(fl) != n:
             raise ValueError("flip_maps needs one entry per crop")

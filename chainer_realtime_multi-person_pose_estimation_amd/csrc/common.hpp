@@ -108,6 +108,11 @@ struct SplitConvShape {
   int32_t splitk;     // 1: the 7x7 raster kernel may split input chunks over workgroups (small launches)
 };
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st);
+// split-K workspace of a stream (conv_big.hip): floats a capture wanted but could not allocate,
+// grow to that size (outside capture; 0 ok), free on stream destruction
+size_t splitk_ws_capture_short(hipStream_t st);
+int splitk_ws_reserve(hipStream_t st);
+void splitk_ws_release(hipStream_t st);
 // co-split halo kernel (conv_halo.hip): tile of tr rows x tc cols per workgroup, nh 1-KiB halo pieces per plane
 struct HaloTiling {
   int32_t tr, tc, tiles_y, tiles_x, nh;

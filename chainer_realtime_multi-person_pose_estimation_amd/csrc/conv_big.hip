@@ -916,20 +916,63 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
 }
 
-// Per-stream split-K workspace (grown on demand, never freed: a captured hipGraph may keep using
-// an older buffer).  nullptr while the stream is capturing and the buffer is too small.
+// Per-stream split-K workspace, owned by the context that owns the stream: grown on demand
+// outside capture, released by splitk_ws_release() when the context destroys its stream.  While
+// the stream is capturing a hipGraph and the buffer is too small the launch cannot allocate, so it
+// records the size it needs and returns nullptr; the capturing caller checks
+// splitk_ws_capture_short() after EndCapture, grows the buffer with splitk_ws_reserve() and
+// captures again, so graph replays pick the same kernels (and sums) as eager runs.
+struct SplitkWs {
+  float* p = nullptr;
+  size_t floats = 0;
+  size_t short_by = 0;  // largest request refused during capture
+  std::vector<float*> retired;  // outgrown buffers: a graph captured earlier may still read them
+};
+static std::mutex g_ws_mu;
+static std::map<hipStream_t, SplitkWs> g_ws;
+
 static float* splitk_ws(hipStream_t st, size_t floats) {
-  static std::mutex mu;
-  static std::map<hipStream_t, std::pair<float*, size_t>> bufs;
-  std::lock_guard<std::mutex> lk(mu);
-  auto& e = bufs[st];
-  if (e.second >= floats) return e.first;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  SplitkWs& e = g_ws[st];
+  if (e.floats >= floats) return e.p;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    e.short_by = std::max(e.short_by, floats);
+    return nullptr;
+  }
   float* p = nullptr;
   if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
-  e = {p, floats};
+  if (e.p) e.retired.push_back(e.p);
+  e.p = p;
+  e.floats = floats;
   return p;
+}
+
+size_t splitk_ws_capture_short(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws.find(st);
+  return it == g_ws.end() ? 0 : it->second.short_by;
+}
+
+int splitk_ws_reserve(hipStream_t st) {
+  size_t need;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    SplitkWs& e = g_ws[st];
+    need = e.short_by;
+    e.short_by = 0;
+    if (need <= e.floats) return 0;
+  }
+  return splitk_ws(st, need) ? 0 : -1;
+}
+
+void splitk_ws_release(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws.find(st);
+  if (it == g_ws.end()) return;
+  if (it->second.p) (void)hipFree(it->second.p);
+  for (float* p : it->second.retired) (void)hipFree(p);
+  g_ws.erase(it);
 }
 
 // Split-K epilogue of conv_m16_bf16x3: out = act(sum over splits (fixed order) + bias), stored

@@ -193,6 +193,7 @@ struct op_cpm_ctx {
   size_t scratch_bytes = 0;
   double* d_gauss = nullptr;
   int gauss_r = 0;
+  int splitk = 1;  // op_cpm_set_batch_invariant(0): small launches may split K (batch-dependent sums)
 };
 
 namespace op {
@@ -264,7 +265,7 @@ int cpm_geometry(op_cpm_ctx* c, int n, int h, int w) {
   return OP_OK;
 }
 
-SplitConvShape cshape(int n, const CAct& in, const CAct& out, int c16, int ks, bool relu) {
+SplitConvShape cshape(int n, const CAct& in, const CAct& out, int c16, int ks, bool relu, int splitk) {
   SplitConvShape s;
   s.n = n;
   s.h = out.h;
@@ -279,7 +280,7 @@ SplitConvShape cshape(int n, const CAct& in, const CAct& out, int c16, int ks, b
   s.groups = 1;
   s.cs_out32 = 0;
   s.halo_mode = 4;
-  s.splitk = 1;
+  s.splitk = splitk;
   return s;
 }
 
@@ -296,7 +297,7 @@ int cconv(op_cpm_ctx* c, const CAct& in, int cin_off, const CAct& out, int cout_
   g[0].out32 = out32 ? out32->p : nullptr;
   g[0].out32_off = 0;
   g[1] = g[0];
-  SplitConvShape s = cshape(c->gn, in, out, pc.cin16 / 16, pc.ks, relu);
+  SplitConvShape s = cshape(c->gn, in, out, pc.cin16 / 16, pc.ks, relu, c->splitk);
   if (out32) s.cs_out32 = out32->cs;
   return launch_conv_bf16x3(s, g, c->stream);
 }
@@ -314,7 +315,7 @@ int cconv_pool(op_cpm_ctx* c, const CAct& in, const CAct& full, const CAct& pool
   g[0].out32 = nullptr;
   g[0].out32_off = 0;
   g[1] = g[0];
-  SplitConvShape s = cshape(c->gn, in, full, pc.cin16 / 16, pc.ks, true);
+  SplitConvShape s = cshape(c->gn, in, full, pc.cin16 / 16, pc.ks, true, c->splitk);
   s.pout = pooled.pad;
   s.cs_out = pooled.cs;
   int taken = 0;
@@ -467,6 +468,12 @@ static void cpm_free_weights(op_cpm_ctx* c) {
   c->have_weights = false;
 }
 
+int op_cpm_set_batch_invariant(op_cpm_ctx* c, int32_t enable) {
+  CRC(cpm_check(c, false));
+  c->splitk = enable ? 0 : 1;
+  return OP_OK;
+}
+
 int op_cpm_destroy(op_cpm_ctx* c) {
   if (!c) return OP_OK;
   (void)hipSetDevice(c->device);
@@ -475,6 +482,7 @@ int op_cpm_destroy(op_cpm_ctx* c) {
   if (c->arena) (void)hipFree(c->arena);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->d_gauss) (void)hipFree(c->d_gauss);
+  splitk_ws_release(c->stream);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return OP_OK;
@@ -631,7 +639,8 @@ int op_cpm_detect(op_cpm_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   const int S = 368;  // params['face_inference_img_size'] = params['hand_inference_img_size'] (entity.py:127, 143)
   CRC(cpm_geometry(c, 1, S, S));
   const int lh = S / 8, lw = S / 8, ch = c->nm;
-  const size_t ib = ((size_t)h * row_stride + 255) / 256 * 256;
+  const int64_t packed = (int64_t)w * 3;  // rows are packed on upload (row_stride may span a wider image)
+  const size_t ib = ((size_t)h * packed + 255) / 256 * 256;
   const size_t lb = ((size_t)ch * lh * lw * 4 + 255) / 256 * 256;
   const size_t pb = ((size_t)ch * h * w * 4 + 255) / 256 * 256;
   CRC(cpm_scratch(c, ib + lb + 3 * pb + (size_t)ch * 16));
@@ -639,8 +648,8 @@ int op_cpm_detect(op_cpm_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   uint8_t* dimg = (uint8_t*)s;
   float* low = (float*)(s + ib);
   float* heat = (float*)(s + ib + lb);
-  OP_HIP_CHECK(hipMemcpyAsync(dimg, bgr, (size_t)h * row_stride, hipMemcpyHostToDevice, c->stream));
-  CRC(launch_preprocess_split(dimg, 0, row_stride, 1, h, w, S, S, c->buf[X0].p, c->stream, 256.0f));
+  OP_HIP_CHECK(hipMemcpy2DAsync(dimg, packed, bgr, row_stride, packed, h, hipMemcpyHostToDevice, c->stream));
+  CRC(launch_preprocess_split(dimg, 0, packed, 1, h, w, S, S, c->buf[X0].p, c->stream, 256.0f));
   CRC(cpm_run(c));
   const int64_t tot = (int64_t)ch * lh * lw;
   hipLaunchKernelGGL(cpm_planar, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->buf[MAP32].p,
@@ -675,7 +684,7 @@ int op_cpm_detect_batch(op_cpm_ctx* c, int32_t n, const uint8_t* const* bgr, con
   size_t off = 0, pb = 0;
   for (int i = 0; i < n; ++i) {
     ioff[i] = off;
-    off += al((size_t)h[i] * row_stride[i]);
+    off += al((size_t)h[i] * w[i] * 3);
     pb = std::max(pb, al((size_t)ch * h[i] * w[i] * 4));
   }
   const size_t lb = al((size_t)n * ch * lh * lw * 4);
@@ -685,8 +694,10 @@ int op_cpm_detect_batch(op_cpm_ctx* c, int32_t n, const uint8_t* const* bgr, con
   char* s = (char*)c->scratch;
   const size_t fx = c->buf[X0].floats(1);
   for (int i = 0; i < n; ++i) {
-    OP_HIP_CHECK(hipMemcpyAsync(s + ioff[i], bgr[i], (size_t)h[i] * row_stride[i], hipMemcpyHostToDevice, c->stream));
-    CRC(launch_preprocess_split((const uint8_t*)(s + ioff[i]), 0, row_stride[i], 1, h[i], w[i], S, S,
+    const int64_t packed = (int64_t)w[i] * 3;
+    OP_HIP_CHECK(hipMemcpy2DAsync(s + ioff[i], packed, bgr[i], row_stride[i], packed, h[i], hipMemcpyHostToDevice,
+                                  c->stream));
+    CRC(launch_preprocess_split((const uint8_t*)(s + ioff[i]), 0, packed, 1, h[i], w[i], S, S,
                                 c->buf[X0].p + (size_t)i * fx, c->stream, 256.0f));
   }
   CRC(cpm_run(c));

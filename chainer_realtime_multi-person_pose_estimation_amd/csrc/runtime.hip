@@ -1047,7 +1047,11 @@ int op_destroy(op_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
-  if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    splitk_ws_release(c->stream);
+    hipStreamDestroy(c->stream);
+  }
   delete c;
   return OP_OK;
 }
@@ -1582,7 +1586,7 @@ int op_run_staged_graph(op_ctx* c) {
   // the graph bakes in every pointer and size: replay only if none changed since capture
   const uintptr_t key[10] = {(uintptr_t)c->st_n, (uintptr_t)c->st_h, (uintptr_t)c->st_w, (uintptr_t)c->use_maps,
                              (uintptr_t)c->arena, (uintptr_t)c->post_arena, (uintptr_t)c->d_frames,
-                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw) * 2 + (uintptr_t)c->split};
+                             (uintptr_t)c->d_maps, (uintptr_t)c->gn, (uintptr_t)(c->gh * 65536 + c->gw) * 4 + (uintptr_t)c->split * 2 + (uintptr_t)c->splitk};
   if (c->gexec && memcmp(key, c->g_key, sizeof(key)) != 0) {
     hipGraphExecDestroy(c->gexec);
     c->gexec = nullptr;
@@ -1596,16 +1600,29 @@ int op_run_staged_graph(op_ctx* c) {
       hipGraphDestroy(c->graph);
       c->graph = nullptr;
     }
-    OP_HIP_CHECK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_staged(c, false);
-    c->prof = prof;
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(c->stream, &g);
-    if (rc) {
-      if (g) hipGraphDestroy(g);
-      return rc;
+    for (int attempt = 0;; ++attempt) {
+      OP_HIP_CHECK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      int rc = enqueue_staged(c, false);
+      hipError_t e = hipStreamEndCapture(c->stream, &g);
+      if (rc || e != hipSuccess) {
+        c->prof = prof;
+        if (g) hipGraphDestroy(g);
+        if (rc) return rc;
+        OP_HIP_CHECK(e);
+      }
+      // a split-K launch that found its workspace too small during capture ran unsplit: grow the
+      // workspace outside capture and capture again, so replays match eager runs
+      if (splitk_ws_capture_short(c->stream) == 0) break;
+      hipGraphDestroy(g);
+      g = nullptr;
+      if (attempt > 0 || splitk_ws_reserve(c->stream) != 0) {
+        c->prof = prof;
+        set_error("split-K workspace allocation failed");
+        return OP_ERR_HIP;
+      }
     }
-    OP_HIP_CHECK(e);
+    c->prof = prof;
     c->graph = g;
     OP_HIP_CHECK(hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
     if (const char* d = getenv("OP_GRAPH_DUMP")) {  // debugging aid: DOT dump of every captured graph
@@ -1910,7 +1927,13 @@ int op_set_precision(op_ctx* c, int32_t mode) {
 int op_set_batch_invariant(op_ctx* c, int32_t enable) {
   using namespace op;
   RC(check_ctx(c, false));
-  c->splitk = enable ? 0 : 1;
+  const int sk = enable ? 0 : 1;
+  if (sk != c->splitk && c->gexec) {  // captured launches bake in the split-K choice
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  c->splitk = sk;
   return OP_OK;
 }
 

@@ -262,6 +262,9 @@ int op_cpm_detect(op_cpm_ctx* ctx, const uint8_t* bgr, int32_t h, int32_t w, int
 int op_cpm_detect_batch(op_cpm_ctx* ctx, int32_t n, const uint8_t* const* bgr, const int32_t* h, const int32_t* w,
                         const int64_t* row_stride, float thresh, const int32_t* flip_maps, double* keypoints,
                         int32_t* found);
+/* enable != 0: no split-K on small launches, so a crop's result does not depend on how many crops
+ * share its batch (op_cpm_detect_batch == op_cpm_detect bit for bit).  Like op_set_batch_invariant. */
+int op_cpm_set_batch_invariant(op_cpm_ctx* ctx, int32_t enable);
 
 /* ---- Training iteration: Updater.update_core of train_coco_pose_estimation.py:93-123 ----
  * One context = CocoPoseNet master weights (f32), Adam state and every activation of a batch of n

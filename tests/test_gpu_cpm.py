@@ -106,6 +106,27 @@ def test_cpm_detect_batch_equals_single_calls(cpm):
     assert c.detect_batch([], 0.1) == []
     with pytest.raises(ValueError):
         c.detect_batch([crops[0], crops[1][:1]], 0.1)  # a 1-row crop: rejected like op_cpm_detect
+    # batch-invariant mode: no split-K, so the batch equals the single calls bit for bit
+    c.set_batch_invariant(True)
+    try:
+        single = [c.detect(im, 0.05, flip_maps=f) for im, f in zip(crops, flips)]
+        _same(c.detect_batch(crops, 0.05, flip_maps=flips), single)
+    finally:
+        c.set_batch_invariant(False)
+
+
+def test_cpm_detect_strided_crop_views(cpm):
+    """Crops that are views into a larger image (row stride > 3 * width) are uploaded row by row:
+    the same result as a packed copy (op_cpm_detect / op_cpm_detect_batch row_stride)."""
+    arch, c, _ = cpm
+    big = np.random.default_rng(12).integers(0, 256, (200, 300, 3), dtype=np.uint8)
+    views = [big[10:110, 20:97], big[50:190, 150:299], big[:41, :33]]
+    for v in views:
+        assert v.strides[0] == 900 and not v.flags.c_contiguous
+        _same(c.detect(v, 0.05), c.detect(np.ascontiguousarray(v), 0.05))
+    got = c.detect_batch(views, 0.05)
+    exp = c.detect_batch([np.ascontiguousarray(v) for v in views], 0.05)
+    _same(got, exp)
 
 
 def test_face_and_hand_detector_api():
@@ -139,6 +160,10 @@ def test_demo_on_golden_poses(tmp_path):
 
     fd = pkg_module("face_detector").FaceDetector("facenet", model=W.random_weights(2, arch="facenet"))
     hd = pkg_module("hand_detector").HandDetector("handnet", model=W.random_weights(2, arch="handnet"))
+    # batch-invariant mode: the batched crops and the per-crop calls sum in the same order, so the
+    # drawn images are equal by construction, not by the absence of near-ties
+    fd._ctx.set_batch_invariant(True)
+    hd._ctx.set_batch_invariant(True)
     img = people_image()
     log = []
     out = demo.run(img, Pose(), fd, hd, log=log.append)
