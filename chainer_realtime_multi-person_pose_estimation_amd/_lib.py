@@ -24,7 +24,7 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
-    "op_set_precision", "op_get_precision", "op_fetch_results", "op_detect_precise", "op_resize_cubic",
+    "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
@@ -120,6 +120,7 @@ def lib():
         "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect_batch": ([P, I32, P, P, P, P, ctypes.c_float, P, P, P], ctypes.c_int),
+        "op_fetch_maps": ([P, I32, I32, P, P, P, P], ctypes.c_int),
         "op_cpm_set_batch_invariant": ([P, I32], ctypes.c_int),
         "op_train_create": ([I32, I32, I32, I32, P], ctypes.c_int),
         "op_train_destroy": ([P], ctypes.c_int),
@@ -261,8 +262,11 @@ class Context(object):
         if img.ndim != 3 or img.shape[2] != 3:
             raise ValueError("expected an H x W x 3 uint8 BGR image")
         poses, scores, res = self._result_arrays(cap)
-        check(lib().op_detect(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], ptr(poses), ptr(scores),
-                              cap, ctypes.byref(res)), "op_detect")
+        rc = lib().op_detect(self.h, ptr(img), img.shape[0], img.shape[1], img.strides[0], ptr(poses), ptr(scores),
+                             cap, ctypes.byref(res))
+        if rc == OP_ERR_CAPACITY and res.n_persons > cap:  # more persons than rows: the frame stays staged
+            return self.fetch_result(0, cap=res.n_persons)
+        check(rc, "op_detect")
         return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
 
     def set_conv_algo(self, algo):
@@ -286,6 +290,9 @@ class Context(object):
         rc = lib().op_detect_precise(self.h, ptr(img), h, w, img.strides[0], ptr(poses), ptr(scores), cap,
                                      ctypes.byref(res), ptr(pafs) if return_maps else None,
                                      ptr(heat) if return_maps else None)
+        if rc == OP_ERR_CAPACITY and res.n_persons > cap:  # more persons than rows: the frame stays staged
+            out = self.fetch_result(0, cap=res.n_persons)
+            return out + (pafs, heat) if return_maps else out
         try:
             check(rc, "op_detect_precise")
         except IndexError as e:  # the averaged maps are valid: keep them for inspection
@@ -349,22 +356,31 @@ class Context(object):
         heatmaps = np.ascontiguousarray(heatmaps, dtype=np.float32)
         c, h, w = heatmaps.shape
         cap = max(1, N_JOINTS * 2048)
-        out = np.empty((cap, 5), np.float64)
-        n = ctypes.c_int64()
-        check(lib().op_compute_peaks(self.h, ptr(heatmaps), c, h, w, ptr(out), cap, ctypes.byref(n)),
-              "op_compute_peaks")
-        return out[:n.value].copy()
+        while True:  # uncapped: on a too-small array the library reports the rows it needs
+            out = np.empty((cap, 5), np.float64)
+            n = ctypes.c_int64()
+            rc = lib().op_compute_peaks(self.h, ptr(heatmaps), c, h, w, ptr(out), cap, ctypes.byref(n))
+            if rc == OP_ERR_CAPACITY and n.value > cap:
+                cap = n.value
+                continue
+            check(rc, "op_compute_peaks")
+            return out[:n.value].copy()
 
     def compute_connections(self, pafs, peaks, img_len):
         pafs = np.ascontiguousarray(pafs, dtype=np.float32)
         peaks = np.ascontiguousarray(np.asarray(peaks, np.float64).reshape(-1, 5))
         _, h, w = pafs.shape
         cap = max(1, N_LIMBS * 2048)
-        conn = np.empty((cap, 3), np.float64)
-        off = np.zeros(N_LIMBS + 1, np.int64)
-        check(lib().op_compute_connections(self.h, ptr(pafs), h, w, ptr(peaks), len(peaks), float(img_len), ptr(conn),
-                                           cap, ptr(off)), "op_compute_connections")
-        return [conn[off[l]:off[l + 1]].copy() for l in range(N_LIMBS)]
+        while True:
+            conn = np.empty((cap, 3), np.float64)
+            off = np.zeros(N_LIMBS + 1, np.int64)
+            rc = lib().op_compute_connections(self.h, ptr(pafs), h, w, ptr(peaks), len(peaks), float(img_len),
+                                              ptr(conn), cap, ptr(off))
+            if rc == OP_ERR_CAPACITY and off[N_LIMBS] > cap:
+                cap = int(off[N_LIMBS])
+                continue
+            check(rc, "op_compute_connections")
+            return [conn[off[l]:off[l + 1]].copy() for l in range(N_LIMBS)]
 
     def grouping(self, connections, peaks):
         peaks = np.ascontiguousarray(np.asarray(peaks, np.float64).reshape(-1, 5))
@@ -373,20 +389,31 @@ class Context(object):
         off = np.zeros(N_LIMBS + 1, np.int64)
         off[1:] = np.cumsum([len(r) for r in rows])
         cap = 2048
-        subsets = np.empty((cap, 20), np.float64)
-        n = ctypes.c_int64()
-        check(lib().op_grouping(self.h, ptr(conn if len(conn) else np.zeros((1, 3))), ptr(off), ptr(peaks), len(peaks),
-                                ptr(subsets), cap, ctypes.byref(n)), "op_grouping")
-        return subsets[:n.value].copy()
+        cptr = conn if len(conn) else np.zeros((1, 3))
+        while True:
+            subsets = np.empty((cap, 20), np.float64)
+            n = ctypes.c_int64()
+            rc = lib().op_grouping(self.h, ptr(cptr), ptr(off), ptr(peaks), len(peaks), ptr(subsets), cap,
+                                   ctypes.byref(n))
+            if rc == OP_ERR_CAPACITY and n.value > cap:
+                cap = n.value
+                continue
+            check(rc, "op_grouping")
+            return subsets[:n.value].copy()
 
     def postprocess(self, paf_low, heat_low, orig_h, orig_w, cap=2048):
         paf_low = np.ascontiguousarray(paf_low, dtype=np.float32)
         heat_low = np.ascontiguousarray(heat_low, dtype=np.float32)
         _, h, w = paf_low.shape
-        poses, scores, res = self._result_arrays(cap)
-        check(lib().op_postprocess(self.h, ptr(paf_low), ptr(heat_low), h, w, int(orig_h), int(orig_w), ptr(poses),
-                                   ptr(scores), cap, ctypes.byref(res)), "op_postprocess")
-        return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+        while True:
+            poses, scores, res = self._result_arrays(cap)
+            rc = lib().op_postprocess(self.h, ptr(paf_low), ptr(heat_low), h, w, int(orig_h), int(orig_w),
+                                      ptr(poses), ptr(scores), cap, ctypes.byref(res))
+            if rc == OP_ERR_CAPACITY and res.n_persons > cap:
+                cap = res.n_persons
+                continue
+            check(rc, "op_postprocess")
+            return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
 
     # ---- staged batched path ----
     def stage_frames(self, frames):
@@ -415,19 +442,41 @@ class Context(object):
         check(lib().op_synchronize(self.h), "op_synchronize")
 
     def fetch_result(self, frame, cap=2048):
-        poses, scores, res = self._result_arrays(cap)
-        check(lib().op_fetch_result(self.h, int(frame), ptr(poses), ptr(scores), cap, ctypes.byref(res)),
-              "op_fetch_result")
-        return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
+        while True:
+            poses, scores, res = self._result_arrays(cap)
+            rc = lib().op_fetch_result(self.h, int(frame), ptr(poses), ptr(scores), cap, ctypes.byref(res))
+            if rc == OP_ERR_CAPACITY and res.n_persons > cap:
+                cap = res.n_persons
+                continue
+            check(rc, "op_fetch_result")
+            return poses[:res.n_persons].copy(), scores[:res.n_persons].copy(), res
 
     def fetch_results(self, first, n, cap=64):
         """Results of staged frames [first, first+n) in three copies: [(poses, scores, res), ...]."""
-        poses = np.empty((n, cap, N_JOINTS, 3), np.float64)
-        scores = np.empty((n, cap), np.float64)
-        res = (OpFrameResult * n)()
-        check(lib().op_fetch_results(self.h, int(first), int(n), ptr(poses), ptr(scores), cap, res),
-              "op_fetch_results")
+        while True:
+            poses = np.empty((n, cap, N_JOINTS, 3), np.float64)
+            scores = np.empty((n, cap), np.float64)
+            res = (OpFrameResult * n)()
+            rc = lib().op_fetch_results(self.h, int(first), int(n), ptr(poses), ptr(scores), cap, res)
+            most = max(r.n_persons for r in res)
+            if rc == OP_ERR_CAPACITY and most > cap:
+                cap = most
+                continue
+            check(rc, "op_fetch_results")
+            break
         return [(poses[i, :res[i].n_persons].copy(), scores[i, :res[i].n_persons].copy(), res[i]) for i in range(n)]
+
+    def fetch_maps(self, first=0, n=1):
+        """Network maps of staged frames [first, first+n): (pafs (n,38,h,w), heatmaps (n,19,h,w)) --
+        the last-stage maps of run_staged, or the averaged full-resolution maps of run_staged_precise."""
+        mh, mw = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().op_fetch_maps(self.h, int(first), int(n), None, None, ctypes.byref(mh), ctypes.byref(mw)),
+              "op_fetch_maps")
+        pafs = np.empty((n, N_PAF, mh.value, mw.value), np.float32)
+        heat = np.empty((n, N_HEAT, mh.value, mw.value), np.float32)
+        check(lib().op_fetch_maps(self.h, int(first), int(n), ptr(pafs), ptr(heat), ctypes.byref(mh),
+                                  ctypes.byref(mw)), "op_fetch_maps")
+        return pafs, heat
 
     def last_timing(self):
         a, b, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <type_traits>
 
 #include "openpose_hip.h"
 
@@ -206,6 +207,7 @@ struct PostBuffers {
   double* res_subsets; // [B][maxs][20] kept subset rows (grouping_key_points output)
   int32_t* res_hdr;    // [B][4]: status, n_peaks, n_persons, reserved
   double* gauss_w;     // [21] device copy of the Gaussian taps
+  unsigned* used;      // big mode only (else null): [B][19][2][ceil(maxp/32)] greedy used-peak bitsets
 };
 
 struct PostShape {

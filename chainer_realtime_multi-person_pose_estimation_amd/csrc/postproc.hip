@@ -214,8 +214,11 @@ __global__ __launch_bounds__(256) void limb_pairs_full(const float* __restrict__
 // peaks are both unused, until min(|A|,|B|) connections (pose_detector.py:172-177).  Accepting
 // the (score desc, index asc) maximum among still-valid candidates is exactly first-fit over
 // the stably sorted list: every skipped candidate keeps a used endpoint forever.
+// kBig: the used-peak bitsets live in HBM (b.used, [frame][limb][2][words]) for any peak count;
+// otherwise in LDS (maxp <= 2048).
+template <bool kBig>
 __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
-  __shared__ unsigned used_a[64], used_b[64];  // maxp <= 2048
+  __shared__ unsigned used_lds[kBig ? 1 : 128];
   __shared__ double red_s[4];
   __shared__ int red_i[4];
   const int f = blockIdx.x, l = blockIdx.y;
@@ -233,7 +236,11 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
     if (j < ja) base_a += c;
     if (j < jb) base_b += c;
   }
-  for (int i = tid; i < 64; i += 256) {
+  const int words = kBig ? (b.maxp + 31) / 32 : 64;
+  unsigned* used_a = used_lds;
+  if constexpr (kBig) used_a = b.used + fl * 2 * words;
+  unsigned* used_b = used_a + (kBig ? words : 64);
+  for (int i = tid; i < words; i += 256) {
     used_a[i] = 0;
     used_b[i] = 0;
   }
@@ -295,12 +302,26 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
 }
 
 // grouping_key_points + subsets_to_pose_array, one wave per frame.
+// kBig: the subsets live in HBM (b.sub_ids / b.sub_sc, b.maxs rows, int32 peak ids) for any
+// peak and subset count; otherwise in LDS (<= kMaxSubsetsLds rows, int16 ids).
+template <bool kBig>
 __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
-  __shared__ int16_t ids[kMaxSubsetsLds][OP_N_JOINTS];
-  __shared__ double sc[kMaxSubsetsLds][2];
+  using IdT = typename std::conditional<kBig, int32_t, int16_t>::type;
+  constexpr int kRows = kBig ? 1 : kMaxSubsetsLds;
+  __shared__ int16_t ids_lds[kRows][OP_N_JOINTS];
+  __shared__ double sc_lds[kRows][2];
   __shared__ int base[OP_N_JOINTS + 1];
   __shared__ int cnt[OP_N_JOINTS];
   const int f = blockIdx.x;
+  IdT (*ids)[OP_N_JOINTS];
+  double (*sc)[2];
+  if constexpr (kBig) {
+    ids = (IdT(*)[OP_N_JOINTS])(b.sub_ids + (int64_t)f * b.maxs * OP_N_JOINTS);
+    sc = (double(*)[2])(b.sub_sc + (int64_t)f * b.maxs * 2);
+  } else {
+    ids = ids_lds;
+    sc = sc_lds;
+  }
   const int lane = threadIdx.x;
   if (lane < OP_N_JOINTS) cnt[lane] = b.peak_cnt[(int64_t)f * OP_N_JOINTS + lane];
   __syncthreads();
@@ -349,14 +370,14 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
       }
       if (found == 1) {
         if (lane == 0 && ids[f0][jb] != ib) {
-          ids[f0][jb] = (int16_t)ib;
+          ids[f0][jb] = (IdT)ib;
           sc[f0][1] = __dadd_rn(sc[f0][1], 1.0);
           sc[f0][0] = __dadd_rn(sc[f0][0], __dadd_rn(pscore(jb, ib), score));
         }
       } else if (found == 2) {
         const bool both = lane < OP_N_JOINTS && ids[f0][lane] >= 0 && ids[f1][lane] >= 0;
         if (__ballot(both) == 0ull) {
-          if (lane < OP_N_JOINTS) ids[f0][lane] = (int16_t)(ids[f0][lane] + ids[f1][lane] + 1);
+          if (lane < OP_N_JOINTS) ids[f0][lane] = (IdT)(ids[f0][lane] + ids[f1][lane] + 1);
           if (lane == 0) {
             sc[f0][0] = __dadd_rn(sc[f0][0], sc[f1][0]);
             sc[f0][1] = __dadd_rn(sc[f0][1], sc[f1][1]);
@@ -367,7 +388,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
           // np.delete(subsets, f1): shift rows down, 64 rows per step (read all, then write)
           for (int r0 = f1; r0 < S - 1; r0 += 64) {
             const int r = r0 + lane;
-            int16_t row[OP_N_JOINTS];
+            IdT row[OP_N_JOINTS];
             double s2[2];
             const bool act = r < S - 1;
             if (act) {
@@ -389,22 +410,22 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
           for (int q = 0; q < 2; ++q) {
             const int t = fs[q];
             if (ids[t][ja] == -1) {
-              ids[t][ja] = (int16_t)ia;
+              ids[t][ja] = (IdT)ia;
               sc[t][1] = __dadd_rn(sc[t][1], 1.0);
               sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(pscore(ja, ia), score));
             } else if (ids[t][jb] == -1) {
-              ids[t][jb] = (int16_t)ib;
+              ids[t][jb] = (IdT)ib;
               sc[t][1] = __dadd_rn(sc[t][1], 1.0);
               sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(pscore(jb, ib), score));
             }
           }
         }
       } else if (l != 9 && l != 13) {
-        if (S >= kMaxSubsetsLds || S >= b.maxs) {
+        if ((!kBig && S >= kMaxSubsetsLds) || S >= b.maxs) {
           status = OP_ERR_CAPACITY;
           break;
         }
-        if (lane < OP_N_JOINTS) ids[S][lane] = (int16_t)(lane == ja ? ia : (lane == jb ? ib : -1));
+        if (lane < OP_N_JOINTS) ids[S][lane] = (IdT)(lane == ja ? ia : (lane == jb ? ib : -1));
         if (lane == 0) {
           sc[S][1] = 2.0;
           sc[S][0] = __dadd_rn(__dadd_rn(pscore(ja, ia), pscore(jb, ib)), score);
@@ -713,6 +734,35 @@ __global__ __launch_bounds__(512) void peak_sort(const int32_t* __restrict__ sta
   }
 }
 
+// Per (frame, joint), any peak count: each staged peak's rank in y*mw + x order (keys are distinct
+// pixels) counted against every other key through LDS tiles; grid (planes, ceil(cap / 256)).
+__global__ __launch_bounds__(256) void peak_sort_rank(const int32_t* __restrict__ stage_key,
+                                                      const float* __restrict__ stage_score, int cap, int mw,
+                                                      const int32_t* __restrict__ peak_cnt, int32_t* __restrict__ peak_xy,
+                                                      float* __restrict__ peak_score) {
+  __shared__ int32_t tile[2048];
+  const int fj = blockIdx.x;
+  int n = peak_cnt[fj];
+  if (n > cap) n = cap;
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  if ((int)blockIdx.y * 256 >= n) return;  // whole block idle (uniform)
+  const int32_t* keys = stage_key + (int64_t)fj * cap;
+  const int32_t ki = i < n ? keys[i] : 0x7fffffff;
+  int rank = 0;
+  for (int j0 = 0; j0 < n; j0 += 2048) {
+    const int m = n - j0 < 2048 ? n - j0 : 2048;
+    __syncthreads();
+    for (int j = threadIdx.x; j < m; j += 256) tile[j] = keys[j0 + j];
+    __syncthreads();
+    for (int j = 0; j < m; ++j) rank += tile[j] < ki ? 1 : 0;
+  }
+  if (i < n) {
+    const int y = ki / mw, x = ki - y * mw;
+    peak_xy[(int64_t)fj * cap + rank] = x | (y << 16);
+    peak_score[(int64_t)fj * cap + rank] = stage_score[(int64_t)fj * cap + i];
+  }
+}
+
 template <class Src>
 static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
   const int planes = s.n * OP_N_JOINTS;
@@ -725,9 +775,15 @@ static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hi
     hipLaunchKernelGGL((heat_fused<Src, 0>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
                        s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
   OP_AFTER_LAUNCH("heat_fused<Src>", st);
-  hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,
-                     b.peak_cnt, b.peak_xy, b.peak_score);
-  OP_AFTER_LAUNCH("peak_sort", st);
+  if (b.maxp <= 2048) {
+    hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,
+                       b.peak_cnt, b.peak_xy, b.peak_score);
+    OP_AFTER_LAUNCH("peak_sort", st);
+  } else {
+    hipLaunchKernelGGL(peak_sort_rank, dim3((unsigned)planes, (unsigned)((b.maxp + 255) / 256)), dim3(256), 0, st,
+                       b.stage_key, b.stage_score, b.maxp, s.mw, b.peak_cnt, b.peak_xy, b.peak_score);
+    OP_AFTER_LAUNCH("peak_sort_rank", st);
+  }
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -735,8 +791,33 @@ static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hi
 // ---------------- launchers ----------------
 static inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// Big mode (b.used != nullptr: the uncapped re-run of one frame, post_big.cpp-style buffers sized
+// from the frame's own counts): HBM bitsets / subsets, rank sort, more candidate-pair blocks.
+static inline bool big_mode(const PostBuffers& b) { return b.used != nullptr; }
+
+static int launch_greedy(const PostShape& s, PostBuffers& b, hipStream_t st) {
+  if (big_mode(b))
+    hipLaunchKernelGGL(limb_greedy<true>, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
+  else
+    hipLaunchKernelGGL(limb_greedy<false>, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
+  OP_AFTER_LAUNCH("limb_greedy", st);
+  return OP_OK;
+}
+
+static int launch_group(const PostShape& s, PostBuffers& b, hipStream_t st) {
+  if (big_mode(b))
+    hipLaunchKernelGGL(grouping<true>, dim3(s.n), dim3(64), 0, st, s, b);
+  else
+    hipLaunchKernelGGL(grouping<false>, dim3(s.n), dim3(64), 0, st, s, b);
+  OP_AFTER_LAUNCH("grouping", st);
+  return OP_OK;
+}
+
+static inline unsigned pair_blocks(const PostBuffers& b) { return big_mode(b) ? 64u : 8u; }
+
 static int check_shape(const PostShape& s, const PostBuffers& b) {
-  if (s.mw > 0xffff || s.mh > 0x7fff || s.n_integ > 16 || s.n_integ < 2 || b.maxp > 2048 || s.radius > kMaxR ||
+  if (s.mw > 0xffff || s.mh > 0x7fff || s.n_integ > 16 || s.n_integ < 2 || (b.maxp > 2048 && !big_mode(b)) ||
+      s.radius > kMaxR ||
       s.mh <= s.radius || s.mw <= s.radius || (int64_t)s.mh * s.mw >= 0x7fffffff) {
     set_error("post-process shape outside kernel limits");
     return OP_ERR_INVALID;
@@ -755,12 +836,10 @@ int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, h
   hs.mw = s.mw;
   if ((rc = run_heat_tiled(hs, s, b, st))) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
-  hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, src, s, b);
+  hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, pair_blocks(b)), dim3(256), 0, st, src, s, b);
   OP_AFTER_LAUNCH("limb_pairs_low", st);
-  hipLaunchKernelGGL(limb_greedy, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
-  OP_AFTER_LAUNCH("limb_greedy", st);
-  hipLaunchKernelGGL(grouping, dim3(s.n), dim3(64), 0, st, s, b);
-  OP_AFTER_LAUNCH("grouping", st);
+  if ((rc = launch_greedy(s, b, st))) return rc;
+  if ((rc = launch_group(s, b, st))) return rc;
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -787,10 +866,10 @@ int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const
   int rc = check_shape(s, b);
   if (rc) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
-  hipLaunchKernelGGL(limb_pairs_full, dim3(s.n, OP_N_LIMBS, 8), dim3(256), 0, st, paf_full, fstride, s, b);
+  hipLaunchKernelGGL(limb_pairs_full, dim3(s.n, OP_N_LIMBS, pair_blocks(b)), dim3(256), 0, st, paf_full, fstride, s,
+                     b);
   OP_AFTER_LAUNCH("limb_pairs_full", st);
-  hipLaunchKernelGGL(limb_greedy, dim3(s.n, OP_N_LIMBS), dim3(256), 0, st, s, b);
-  OP_AFTER_LAUNCH("limb_greedy", st);
+  if ((rc = launch_greedy(s, b, st))) return rc;
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }
@@ -798,8 +877,7 @@ int launch_connections_full(const float* paf_full, int32_t mh, int32_t mw, const
 int launch_grouping(const PostShape& s, PostBuffers& b, hipStream_t st) {
   int rc = check_shape(s, b);
   if (rc) return rc;
-  hipLaunchKernelGGL(grouping, dim3(s.n), dim3(64), 0, st, s, b);
-  OP_AFTER_LAUNCH("grouping", st);
+  if ((rc = launch_group(s, b, st))) return rc;
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
 }

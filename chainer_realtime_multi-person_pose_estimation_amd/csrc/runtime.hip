@@ -211,6 +211,16 @@ struct Act {
   size_t frame_floats() const { return (size_t)(h + 2 * pad) * (w + 2 * pad) * cs; }
 };
 
+// Input of the last batched post-process (0: none, 1: low-res maps through the fused upsample,
+// 2: full-resolution planar maps of the precise path), kept so one frame can be re-run uncapped.
+struct PostRecord {
+  int kind = 0;
+  MapSource low{};
+  const float* full = nullptr;
+  int64_t fstride = 0;
+  PostShape s{};
+};
+
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
   B_S1, B_MAP32, B_COUNT
@@ -269,6 +279,9 @@ struct op_ctx {
   float* d_maps = nullptr;
   size_t maps_bytes = 0;
   int sm_n = 0, sm_h = 0, sm_w = 0;
+  float* d_fmaps = nullptr;  // staged full-resolution maps for the precise post-process, planar (n, 57, h, w)
+  size_t fmaps_bytes = 0;
+  int fm_n = 0, fm_h = 0, fm_w = 0;
   bool use_maps = false;
   float* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -296,6 +309,12 @@ struct op_ctx {
   // pinned host staging for batched result fetches
   char* host_stage = nullptr;
   size_t host_stage_bytes = 0;
+  // uncapped post-process: the last batched post-process's input (to re-run one frame) and the
+  // one-frame big-mode buffers sized from that frame's own counts
+  op::PostRecord post_rec;
+  PostBuffers bigb{};
+  void* bb_arena = nullptr;
+  int big_frame = -1;  // frame of post_rec whose big-mode result sits in bb
 };
 
 namespace op {
@@ -706,6 +725,7 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
 // followed by heat [6][n][19][lh][lw] (op_forward_stages; the reference's pafs / heatmaps lists).
 static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame_bytes = 0, int64_t row_stride = 0,
                        int sh = 0, int sw = 0, float* stages = nullptr) {
+  c->post_rec.kind = 0;  // the maps a recorded post-process read are overwritten from here on
   Act* B = c->buf;
   const size_t stage_px = (size_t)c->gn * (c->gh / 8) * (c->gw / 8);
   auto dump_stage = [&](int s) -> int {
@@ -835,9 +855,145 @@ static void optimal_size(int h, int w, int img_size, int stride, int* out_w, int
   *out_h = ih;
 }
 
+// ---- uncapped post-process (the reference has no caps, pose_detector.py:75-250) ----
+// A frame whose peaks per joint exceed the batched buffers' cap, or whose subsets overflow the
+// LDS grouping, is re-run alone in "big mode": one-frame buffers sized from its own counts (peaks
+// per joint, candidates per limb, subsets <= connections + 1), greedy bitsets and subsets in HBM,
+// a rank sort for the peak lists.  Only device memory bounds it (OP_ERR_CAPACITY if an allocation
+// fails).
+static int big_buffers(op_ctx* c, int maxp, int64_t maxc, PostBuffers** out) {
+  maxp = std::max(maxp, 1);
+  maxc = std::max<int64_t>(maxc, 1);
+  if (c->bb_arena && c->bigb.maxp >= maxp && c->bigb.maxc >= maxc) {
+    *out = &c->bigb;
+    return OP_OK;
+  }
+  if (c->bb_arena) {
+    maxp = std::max(maxp, c->bigb.maxp);
+    maxc = std::max(maxc, c->bigb.maxc);
+  }
+  if ((int64_t)maxp * maxp >= ((int64_t)1 << 31)) {  // candidate pair indices are int32
+    set_error("more than 46340 peaks for one joint");
+    return OP_ERR_CAPACITY;
+  }
+  PostBuffers b{};
+  b.maxp = maxp;
+  b.maxc = maxc;
+  b.maxs = OP_N_LIMBS * maxp + 1;  // every new subset consumes a connection (<= maxp per limb)
+  const size_t words = ((size_t)maxp + 31) / 32, P = (size_t)maxp, S = (size_t)b.maxs, C = (size_t)maxc;
+  struct Part {
+    void** p;
+    size_t bytes;
+  };
+  const Part parts[] = {
+      {(void**)&b.peak_xy, OP_N_JOINTS * P * 4},   {(void**)&b.peak_score, OP_N_JOINTS * P * 4},
+      {(void**)&b.peak_cnt, OP_N_JOINTS * 4},      {(void**)&b.stage_key, OP_N_JOINTS * P * 4},
+      {(void**)&b.stage_score, OP_N_JOINTS * P * 4}, {(void**)&b.cand_score, OP_N_LIMBS * C * 8},
+      {(void**)&b.cand_idx, OP_N_LIMBS * C * 4},   {(void**)&b.cand_cnt, OP_N_LIMBS * 4},
+      {(void**)&b.conn_ab, OP_N_LIMBS * P * 8},    {(void**)&b.conn_score, OP_N_LIMBS * P * 8},
+      {(void**)&b.conn_cnt, OP_N_LIMBS * 4},       {(void**)&b.sub_ids, S * OP_N_JOINTS * 4},
+      {(void**)&b.sub_sc, S * 2 * 8},              {(void**)&b.res_poses, S * OP_N_JOINTS * 3 * 8},
+      {(void**)&b.res_scores, S * 8},              {(void**)&b.res_subsets, S * 20 * 8},
+      {(void**)&b.res_hdr, 4 * 4},                 {(void**)&b.gauss_w, 64 * 8},
+      {(void**)&b.used, OP_N_LIMBS * 2 * words * 4},
+  };
+  size_t total = 0;
+  for (const Part& q : parts) total += (q.bytes + 255) / 256 * 256;
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->bb_arena) OP_HIP_CHECK(hipFree(c->bb_arena));
+  c->bb_arena = nullptr;
+  c->bigb = PostBuffers{};
+  c->big_frame = -1;
+  if (hipMalloc(&c->bb_arena, total) != hipSuccess) {
+    (void)hipGetLastError();
+    c->bb_arena = nullptr;
+    set_error("post-process of a frame needs more device memory than is free (" + std::to_string(total >> 20) +
+              " MiB for " + std::to_string(maxp) + " peaks per joint)");
+    return OP_ERR_CAPACITY;
+  }
+  char* p = (char*)c->bb_arena;
+  for (const Part& q : parts) {
+    *q.p = p;
+    p += (q.bytes + 255) / 256 * 256;
+  }
+  OP_HIP_CHECK(hipMemcpy(b.gauss_w, c->pb.gauss_w, 64 * 8, hipMemcpyDeviceToDevice));
+  c->bigb = b;
+  *out = &c->bigb;
+  return OP_OK;
+}
+
+// Run the post-process of `peaks` (frame 0 of B) from the recorded input of frame f.
+static int post_one_frame(op_ctx* c, const PostRecord& r, int f, PostBuffers& B) {
+  PostShape s1 = r.s;
+  s1.n = 1;
+  if (r.kind == 1) {
+    MapSource src = r.low;
+    src.base += (int64_t)f * src.fstride;
+    return launch_post_maps(src, s1, B, c->stream);
+  }
+  const float* m = r.full + (int64_t)f * r.fstride;
+  RC(launch_peaks_from_full(m + (size_t)OP_N_PAF * s1.mh * s1.mw, OP_N_JOINTS, s1.mh, s1.mw, s1, B, c->stream,
+                            r.fstride));
+  RC(launch_connections_full(m, s1.mh, s1.mw, s1, B, c->stream, r.fstride));
+  return launch_grouping(s1, B, c->stream);
+}
+
+// Re-run frame f of the last batched post-process in big mode; *out = buffers holding its result.
+static int rerun_big(op_ctx* c, int f, PostBuffers** out) {
+  if (c->big_frame == f && c->bb_arena) {
+    *out = &c->bigb;
+    return OP_OK;
+  }
+  const PostRecord r = c->post_rec;
+  if (r.kind == 0 || f < 0 || f >= r.s.n) {
+    set_error("post-process capacity exceeded and no recorded input to re-run the frame");
+    return OP_ERR_CAPACITY;
+  }
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  int32_t cnt[OP_N_JOINTS];
+  OP_HIP_CHECK(hipMemcpy(cnt, c->pb.peak_cnt + (size_t)f * OP_N_JOINTS, sizeof(cnt), hipMemcpyDeviceToHost));
+  int maxp = 1;
+  for (int j = 0; j < OP_N_JOINTS; ++j) maxp = std::max(maxp, cnt[j]);
+  int64_t maxc = std::min<int64_t>((int64_t)maxp * maxp, (int64_t)1 << 20);
+  PostBuffers* B = nullptr;
+  for (;;) {
+    RC(big_buffers(c, maxp, maxc, &B));
+    RC(post_one_frame(c, r, f, *B));
+    int32_t cc[OP_N_LIMBS];
+    OP_HIP_CHECK(hipMemcpyAsync(cc, B->cand_cnt, sizeof(cc), hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    int64_t need = 0;
+    for (int l = 0; l < OP_N_LIMBS; ++l) need = std::max<int64_t>(need, cc[l]);
+    if (need <= B->maxc) break;
+    maxc = need;  // more candidates than the first guess: grow and run again
+  }
+  c->big_frame = f;
+  *out = B;
+  return OP_OK;
+}
+
+static void post_record(op_ctx* c, int kind, const MapSource* low, const float* full, int64_t fstride,
+                        const PostShape& s) {
+  c->post_rec.kind = kind;
+  if (low) c->post_rec.low = *low;
+  c->post_rec.full = full;
+  c->post_rec.fstride = fstride;
+  c->post_rec.s = s;
+  c->big_frame = -1;
+}
+
 static int read_result(op_ctx* c, int frame, double* poses, double* scores, int cap, op_frame_result* res) {
   int32_t hdr[4];
   OP_HIP_CHECK(hipMemcpy(hdr, c->pb.res_hdr + 4 * frame, sizeof(hdr), hipMemcpyDeviceToHost));
+  const PostBuffers* B = &c->pb;
+  int slot = frame;
+  if (hdr[0] == OP_ERR_CAPACITY && c->post_rec.kind) {  // over the batched caps: re-run uncapped
+    PostBuffers* big = nullptr;
+    RC(rerun_big(c, frame, &big));
+    OP_HIP_CHECK(hipMemcpy(hdr, big->res_hdr, sizeof(hdr), hipMemcpyDeviceToHost));
+    B = big;
+    slot = 0;
+  }
   res->status = hdr[0];
   res->n_peaks = hdr[1];
   res->n_persons = hdr[2];
@@ -851,9 +1007,9 @@ static int read_result(op_ctx* c, int frame, double* poses, double* scores, int 
     return OP_ERR_CAPACITY;
   }
   if (hdr[2] > 0) {
-    OP_HIP_CHECK(hipMemcpy(poses, c->pb.res_poses + (size_t)frame * c->pb.maxs * 54, (size_t)hdr[2] * 54 * 8,
+    OP_HIP_CHECK(hipMemcpy(poses, B->res_poses + (size_t)slot * B->maxs * 54, (size_t)hdr[2] * 54 * 8,
                            hipMemcpyDeviceToHost));
-    OP_HIP_CHECK(hipMemcpy(scores, c->pb.res_scores + (size_t)frame * c->pb.maxs, (size_t)hdr[2] * 8,
+    OP_HIP_CHECK(hipMemcpy(scores, B->res_scores + (size_t)slot * B->maxs, (size_t)hdr[2] * 8,
                            hipMemcpyDeviceToHost));
   }
   return OP_OK;
@@ -1038,12 +1194,14 @@ int op_destroy(op_ctx* c) {
   if (c->post_arena) hipFree(c->post_arena);
   if (c->d_frames) hipFree(c->d_frames);
   if (c->d_maps) hipFree(c->d_maps);
+  if (c->d_fmaps) hipFree(c->d_fmaps);
   if (c->d_scratch) hipFree(c->d_scratch);
   guard_forget(c->d_pmid, c->pmid_bytes + g_guard);
   guard_forget(c->d_psum, c->psum_bytes + g_guard);
   if (c->d_pmid) hipFree(c->d_pmid);
   if (c->d_psum) hipFree(c->d_psum);
   if (c->host_stage) hipHostFree(c->host_stage);
+  if (c->bb_arena) hipFree(c->bb_arena);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
@@ -1227,13 +1385,10 @@ int op_resize_images(op_ctx* c, const float* x, int32_t ch, int32_t h, int32_t w
   return OP_OK;
 }
 
-// Upload (N,5) all_peaks rows (reference format: ordered by joint, ids = row index) into the
-// per-joint peak arrays of frame 0.
-static int upload_peaks(op_ctx* c, const double* peaks, int64_t n) {
-  using namespace op;
-  const int maxp = c->pb.maxp;
-  std::vector<int32_t> xy((size_t)OP_N_JOINTS * maxp, 0), cnt(OP_N_JOINTS, 0);
-  std::vector<float> sc((size_t)OP_N_JOINTS * maxp, 0.0f);
+// Peaks per joint of (N,5) all_peaks rows (reference format: ordered by joint, ids = row index);
+// OP_ERR_INVALID if the rows are not in that format.
+static int peaks_per_joint(const double* peaks, int64_t n, int32_t* cnt) {
+  for (int j = 0; j < OP_N_JOINTS; ++j) cnt[j] = 0;
   int prev = -1;
   for (int64_t i = 0; i < n; ++i) {
     const double* r = peaks + i * 5;
@@ -1244,17 +1399,41 @@ static int upload_peaks(op_ctx* c, const double* peaks, int64_t n) {
       return OP_ERR_INVALID;
     }
     prev = j;
+    cnt[j]++;
+  }
+  return OP_OK;
+}
+
+// The context's batched post buffers when maxp peaks per joint fit them (and !force_big), else the
+// one-frame big-mode buffers sized for maxp / maxc (uncapped: only device memory bounds them).
+static int pick_buffers(op_ctx* c, int maxp, int64_t maxc, bool force_big, PostBuffers** out) {
+  if (!force_big && maxp <= c->pb.maxp && maxc <= c->pb.maxc) {
+    *out = &c->pb;
+    return OP_OK;
+  }
+  return big_buffers(c, std::max(maxp, c->pb.maxp), std::max<int64_t>(maxc, 1), out);
+}
+
+// Upload all_peaks rows into the per-joint peak arrays of frame 0 of B.
+static int upload_peaks(op_ctx* c, PostBuffers& B, const double* peaks, int64_t n) {
+  using namespace op;
+  const int maxp = B.maxp;
+  std::vector<int32_t> xy((size_t)OP_N_JOINTS * maxp, 0), cnt(OP_N_JOINTS, 0);
+  std::vector<float> sc((size_t)OP_N_JOINTS * maxp, 0.0f);
+  for (int64_t i = 0; i < n; ++i) {
+    const double* r = peaks + i * 5;
+    const int j = (int)r[0];
     if (cnt[j] >= maxp) {
-      set_error("too many peaks for one joint (max_peaks_per_joint)");
-      return OP_ERR_CAPACITY;
+      set_error("internal: peak buffers smaller than the peaks per joint");
+      return OP_ERR_INVALID;
     }
     xy[(size_t)j * maxp + cnt[j]] = (int32_t)r[1] | ((int32_t)r[2] << 16);
     sc[(size_t)j * maxp + cnt[j]] = (float)r[3];
     cnt[j]++;
   }
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_xy, xy.data(), xy.size() * 4, hipMemcpyHostToDevice, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_score, sc.data(), sc.size() * 4, hipMemcpyHostToDevice, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.peak_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(B.peak_xy, xy.data(), xy.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(B.peak_score, sc.data(), sc.size() * 4, hipMemcpyHostToDevice, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(B.peak_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   return OP_OK;
 }
@@ -1271,25 +1450,32 @@ int op_compute_peaks(op_ctx* c, const float* heatmaps, int32_t ch, int32_t h, in
   OP_HIP_CHECK(hipMemcpyAsync(c->pb.up, heatmaps, (size_t)OP_N_JOINTS * h * w * 4, hipMemcpyHostToDevice, c->stream));
   PostShape s;
   post_shape(c, s, 1, h, w, h, w, (double)w, 1.0, 1.0);
-  RC(launch_peaks_from_full(c->pb.up, OP_N_JOINTS, h, w, s, c->pb, c->stream));
-  const int maxp = c->pb.maxp;
-  std::vector<int32_t> cnt(OP_N_JOINTS), xy((size_t)OP_N_JOINTS * maxp);
+  PostBuffers* B = &c->pb;
+  std::vector<int32_t> cnt(OP_N_JOINTS);
+  for (;;) {
+    RC(launch_peaks_from_full(c->pb.up, OP_N_JOINTS, h, w, s, *B, c->stream));
+    OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), B->peak_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    const int most = *std::max_element(cnt.begin(), cnt.end());
+    if (most <= B->maxp) break;
+    RC(pick_buffers(c, most, 1, true, &B));  // more peaks than the cap: again, uncapped
+  }
+  const int maxp = B->maxp;
+  std::vector<int32_t> xy((size_t)OP_N_JOINTS * maxp);
   std::vector<float> sc((size_t)OP_N_JOINTS * maxp);
-  OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), c->pb.peak_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(xy.data(), c->pb.peak_xy, xy.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), c->pb.peak_score, sc.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(xy.data(), B->peak_xy, xy.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), B->peak_score, sc.size() * 4, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  int64_t total = 0;
+  for (int j = 0; j < OP_N_JOINTS; ++j) total += cnt[j];
+  if (total > cap) {  // the caller's rows are too few: report how many are needed
+    *n_peaks = total;
+    set_error("peaks capacity too small");
+    return OP_ERR_CAPACITY;
+  }
   int64_t k = 0;
   for (int j = 0; j < OP_N_JOINTS; ++j) {
-    if (cnt[j] > maxp) {
-      set_error("too many peaks for one joint (max_peaks_per_joint)");
-      return OP_ERR_CAPACITY;
-    }
     for (int i = 0; i < cnt[j]; ++i) {
-      if (k >= cap) {
-        set_error("peaks capacity too small");
-        return OP_ERR_CAPACITY;
-      }
       const int32_t v = xy[(size_t)j * maxp + i];
       double* r = peaks + k * 5;
       r[0] = j;
@@ -1313,33 +1499,45 @@ int op_compute_connections(op_ctx* c, const float* pafs, int32_t h, int32_t w, c
     return OP_ERR_INVALID;
   }
   RC(ensure_post(c, 1, h, w));
-  RC(upload_peaks(c, peaks, n_peaks));
+  int32_t pj[OP_N_JOINTS];
+  RC(peaks_per_joint(peaks, n_peaks, pj));
+  const int most = *std::max_element(pj, pj + OP_N_JOINTS);
   const size_t pb = (size_t)OP_N_PAF * h * w * 4;
   RC(ensure_scratch(c, pb));
   OP_HIP_CHECK(hipMemcpyAsync(c->d_scratch, pafs, pb, hipMemcpyHostToDevice, c->stream));
   PostShape s;
   post_shape(c, s, 1, h, w, h, w, img_len, 1.0, 1.0);
-  RC(launch_connections_full(c->d_scratch, h, w, s, c->pb, c->stream));
-  const int maxp = c->pb.maxp;
-  std::vector<int32_t> cnt(OP_N_LIMBS), ab((size_t)OP_N_LIMBS * maxp * 2), ccnt(OP_N_LIMBS);
+  PostBuffers* B = nullptr;
+  int64_t maxc = std::min<int64_t>((int64_t)most * most, (int64_t)1 << 20);
+  RC(pick_buffers(c, most, most <= c->pb.maxp ? 1 : maxc, false, &B));
+  std::vector<int32_t> ccnt(OP_N_LIMBS);
+  for (;;) {
+    RC(upload_peaks(c, *B, peaks, n_peaks));
+    RC(launch_connections_full(c->d_scratch, h, w, s, *B, c->stream));
+    OP_HIP_CHECK(hipMemcpyAsync(ccnt.data(), B->cand_cnt, ccnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    const int64_t need = *std::max_element(ccnt.begin(), ccnt.end());
+    if (need <= B->maxc) break;
+    RC(pick_buffers(c, most, need, true, &B));  // more candidates than the buffers hold: again
+  }
+  const int maxp = B->maxp;
+  std::vector<int32_t> cnt(OP_N_LIMBS), ab((size_t)OP_N_LIMBS * maxp * 2);
   std::vector<double> sc((size_t)OP_N_LIMBS * maxp);
-  OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), c->pb.conn_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(ccnt.data(), c->pb.cand_cnt, ccnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(ab.data(), c->pb.conn_ab, ab.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), c->pb.conn_score, sc.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(cnt.data(), B->conn_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(ab.data(), B->conn_ab, ab.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  OP_HIP_CHECK(hipMemcpyAsync(sc.data(), B->conn_score, sc.size() * 8, hipMemcpyDeviceToHost, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  int64_t total = 0;
+  for (int l = 0; l < OP_N_LIMBS; ++l) total += cnt[l];
+  if (total > cap) {  // the caller's rows are too few: report how many are needed
+    conn_off[OP_N_LIMBS] = total;
+    set_error("connection capacity too small");
+    return OP_ERR_CAPACITY;
+  }
   int64_t k = 0;
   for (int l = 0; l < OP_N_LIMBS; ++l) {
-    if (ccnt[l] > c->pb.maxc) {
-      set_error("candidate capacity exceeded");
-      return OP_ERR_CAPACITY;
-    }
     conn_off[l] = k;
     for (int i = 0; i < cnt[l]; ++i) {
-      if (k >= cap) {
-        set_error("connection capacity too small");
-        return OP_ERR_CAPACITY;
-      }
       conn[k * 3 + 0] = ab[((size_t)l * maxp + i) * 2];
       conn[k * 3 + 1] = ab[((size_t)l * maxp + i) * 2 + 1];
       conn[k * 3 + 2] = sc[(size_t)l * maxp + i];
@@ -1360,10 +1558,9 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
   }
   // map size is irrelevant for grouping; keep whatever post buffers exist
   RC(ensure_post(c, 1, std::max(c->pmh, 8), std::max(c->pmw, 8)));
-  RC(upload_peaks(c, peaks, n_peaks));
-  const int maxp = c->pb.maxp;
-  std::vector<int32_t> cnt(OP_N_LIMBS, 0), ab((size_t)OP_N_LIMBS * maxp * 2, 0);
-  std::vector<double> sc((size_t)OP_N_LIMBS * maxp, 0.0);
+  int32_t pj[OP_N_JOINTS];
+  RC(peaks_per_joint(peaks, n_peaks, pj));
+  int most = *std::max_element(pj, pj + OP_N_JOINTS);
   // peak id ranges per joint (ids are row indices of all_peaks, grouped by joint)
   int64_t jlo[OP_N_JOINTS], jhi[OP_N_JOINTS];
   for (int j = 0; j < OP_N_JOINTS; ++j) {
@@ -1374,10 +1571,11 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
   for (int64_t i = 0; i < n_peaks; ++i) jhi[(int)peaks[i * 5]] = i;
   for (int l = 0; l < OP_N_LIMBS; ++l) {
     const int64_t k0 = conn_off[l], k1 = conn_off[l + 1];
-    if (k1 - k0 > maxp || k1 < k0) {
-      set_error("too many connections for one limb");
-      return OP_ERR_CAPACITY;
+    if (k1 < k0 || k1 - k0 > 0x7fffffff) {
+      set_error("connection offsets must be non-decreasing");
+      return OP_ERR_INVALID;
     }
+    most = std::max<int64_t>(most, k1 - k0);
     const int ja = c->prm.limbs_point[l][0], jb = c->prm.limbs_point[l][1];
     for (int64_t i = k0; i < k1; ++i) {
       const int64_t ia = (int64_t)conn[i * 3], ib = (int64_t)conn[i * 3 + 1];
@@ -1386,22 +1584,35 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
         return OP_ERR_INVALID;
       }
     }
-    cnt[l] = (int)(k1 - k0);
-    for (int64_t i = k0; i < k1; ++i) {
-      ab[((size_t)l * maxp + (i - k0)) * 2] = (int32_t)conn[i * 3];
-      ab[((size_t)l * maxp + (i - k0)) * 2 + 1] = (int32_t)conn[i * 3 + 1];
-      sc[(size_t)l * maxp + (i - k0)] = conn[i * 3 + 2];
-    }
   }
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_ab, ab.data(), ab.size() * 4, hipMemcpyHostToDevice, c->stream));
-  OP_HIP_CHECK(hipMemcpyAsync(c->pb.conn_score, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, c->stream));
+  PostBuffers* B = nullptr;
+  RC(pick_buffers(c, most, 1, false, &B));
   PostShape s;
   post_shape(c, s, 1, 64, 64, 64, 64, 64.0, 1.0, 1.0);  // map size is unused by grouping
-  RC(launch_grouping(s, c->pb, c->stream));
   int32_t hdr[4];
-  OP_HIP_CHECK(hipMemcpyAsync(hdr, c->pb.res_hdr, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
-  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  for (;;) {
+    RC(upload_peaks(c, *B, peaks, n_peaks));
+    const int maxp = B->maxp;
+    std::vector<int32_t> cnt(OP_N_LIMBS, 0), ab((size_t)OP_N_LIMBS * maxp * 2, 0);
+    std::vector<double> sc((size_t)OP_N_LIMBS * maxp, 0.0);
+    for (int l = 0; l < OP_N_LIMBS; ++l) {
+      const int64_t k0 = conn_off[l], k1 = conn_off[l + 1];
+      cnt[l] = (int)(k1 - k0);
+      for (int64_t i = k0; i < k1; ++i) {
+        ab[((size_t)l * maxp + (i - k0)) * 2] = (int32_t)conn[i * 3];
+        ab[((size_t)l * maxp + (i - k0)) * 2 + 1] = (int32_t)conn[i * 3 + 1];
+        sc[(size_t)l * maxp + (i - k0)] = conn[i * 3 + 2];
+      }
+    }
+    OP_HIP_CHECK(hipMemcpyAsync(B->conn_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, c->stream));
+    OP_HIP_CHECK(hipMemcpyAsync(B->conn_ab, ab.data(), ab.size() * 4, hipMemcpyHostToDevice, c->stream));
+    OP_HIP_CHECK(hipMemcpyAsync(B->conn_score, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, c->stream));
+    RC(launch_grouping(s, *B, c->stream));
+    OP_HIP_CHECK(hipMemcpyAsync(hdr, B->res_hdr, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (hdr[0] != OP_ERR_CAPACITY || B != &c->pb) break;
+    RC(pick_buffers(c, most, 1, true, &B));  // more subsets than the LDS grouping holds: again, in HBM
+  }
   if (hdr[0] == OP_ERR_INDEX) {
     set_error("list assignment index out of range (grouping_key_points)");
     return OP_ERR_INDEX;
@@ -1411,11 +1622,12 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
     return hdr[0];
   }
   if (hdr[2] > cap) {
+    *n_subsets = hdr[2];
     set_error("subsets capacity too small");
     return OP_ERR_CAPACITY;
   }
   if (hdr[2] > 0)
-    OP_HIP_CHECK(hipMemcpy(subsets, c->pb.res_subsets, (size_t)hdr[2] * 20 * 8, hipMemcpyDeviceToHost));
+    OP_HIP_CHECK(hipMemcpy(subsets, B->res_subsets, (size_t)hdr[2] * 20 * 8, hipMemcpyDeviceToHost));
   *n_subsets = hdr[2];
   return OP_OK;
 }
@@ -1423,6 +1635,7 @@ int op_grouping(op_ctx* c, const double* conn, const int64_t* conn_off, const do
 // Pack planar (n, 57, lh, lw) maps [38 paf | 19 heat] into an NHWC (n, lh, lw, 57) device buffer.
 static int stage_maps_dev(op_ctx* c, const float* maps, int n, int lh, int lw, float** out) {
   using namespace op;
+  c->post_rec.kind = 0;  // staged maps are replaced
   const size_t fl = (size_t)n * 57 * lh * lw;
   std::vector<float> t(fl);
   for (int f = 0; f < n; ++f)
@@ -1455,6 +1668,7 @@ int op_postprocess(op_ctx* c, const float* paf_low, const float* heat_low, int32
   MapSource src{dm, (int64_t)57 * h * w, 0, 57, 0, 38};
   PostShape s;
   post_shape(c, s, 1, h, w, map_h, map_w, (double)map_w, (double)orig_w / map_w, (double)orig_h / map_h);
+  post_record(c, 1, &src, nullptr, 0, s);
   RC(launch_post_maps(src, s, c->pb, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   memset(res, 0, sizeof(*res));
@@ -1502,6 +1716,7 @@ static int enqueue_staged(op_ctx* c, bool timing) {
   // 2 x (read + write) Gaussian passes + NMS read, f32
   const double mp = (double)c->st_n * map_h * map_w;
   const double pbytes = 4.0 * ((double)c->st_n * 57 * lh * lw + 18 * mp + 2 * 2 * 18 * mp + 18 * mp);
+  post_record(c, 1, &src, nullptr, 0, s);
   RC(profiled(c, 3, 0.0, pbytes, [&] { return launch_post_maps(src, s, c->pb, c->stream); }));
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[2], c->stream));
   c->timed = timing;
@@ -1538,11 +1753,22 @@ int op_stage_maps(op_ctx* c, const float* maps, int32_t n, int32_t mh, int32_t m
     set_error("op_stage_maps: bad arguments");
     return OP_ERR_INVALID;
   }
-  float* dm;
-  RC(stage_maps_dev(c, maps, n, mh, mw, &dm));
-  c->sm_n = n;
-  c->sm_h = mh;
-  c->sm_w = mw;
+  if (c->st_n > 0 && mh == c->st_h && mw == c->st_w) {
+    // full-resolution maps of the staged frames: the precise post-process input (kept planar)
+    const size_t bytes = (size_t)n * 57 * mh * mw * 4;
+    c->post_rec.kind = 0;  // staged maps are replaced
+    RC(grow_buffer(c, (void**)&c->d_fmaps, &c->fmaps_bytes, bytes, "full_maps"));
+    OP_HIP_CHECK(hipMemcpy(c->d_fmaps, maps, bytes, hipMemcpyHostToDevice));
+    c->fm_n = n;
+    c->fm_h = mh;
+    c->fm_w = mw;
+  } else {
+    float* dm;
+    RC(stage_maps_dev(c, maps, n, mh, mw, &dm));
+    c->sm_n = n;
+    c->sm_h = mh;
+    c->sm_w = mw;
+  }
   if (c->gexec) {
     hipGraphExecDestroy(c->gexec);
     c->gexec = nullptr;
@@ -1675,6 +1901,56 @@ int op_fetch_result(op_ctx* c, int32_t frame, double* poses, double* scores, int
   return read_result(c, frame, poses, scores, cap, res);
 }
 
+int op_fetch_maps(op_ctx* c, int32_t first, int32_t n, float* pafs, float* heatmaps, int32_t* mh, int32_t* mw) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (first < 0 || n < 1 || first + n > c->st_n || !mh || !mw) {
+    set_error("op_fetch_maps: bad range");
+    return OP_ERR_INVALID;
+  }
+  int in_w, in_h, map_w, map_h;
+  staged_sizes(c, &in_w, &in_h, &map_w, &map_h);
+  const int h = c->st_precise ? c->st_h : in_h / 8, w = c->st_precise ? c->st_w : in_w / 8;
+  *mh = h;
+  *mw = w;
+  if (!pafs && !heatmaps) return OP_OK;  // size query
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  const size_t hw = (size_t)h * w;
+  if (c->st_precise) {  // the averaged maps: planar (57, h, w) per frame
+    const size_t fpl = (size_t)(OP_N_PAF + OP_N_HEAT) * hw;
+    for (int i = 0; i < n; ++i) {
+      const float* f = c->d_psum + (size_t)(first + i) * fpl;
+      if (pafs) OP_HIP_CHECK(hipMemcpy(pafs + (size_t)i * OP_N_PAF * hw, f, OP_N_PAF * hw * 4, hipMemcpyDeviceToHost));
+      if (heatmaps)
+        OP_HIP_CHECK(hipMemcpy(heatmaps + (size_t)i * OP_N_HEAT * hw, f + OP_N_PAF * hw, OP_N_HEAT * hw * 4,
+                               hipMemcpyDeviceToHost));
+    }
+    return OP_OK;
+  }
+  // single scale: the last-stage maps (NHWC) as the network wrote them
+  const Act& m = c->split ? c->buf[B_MAP32] : c->buf[B_CAT];
+  if (c->gn < first + n || m.h != h || m.w != w) {
+    set_error("op_fetch_maps: no network maps of the staged frames (run op_run_staged first)");
+    return OP_ERR_STATE;
+  }
+  const int paf_off = c->split ? 0 : kCatPaf, heat_off = c->split ? 40 : kCatHeat;
+  std::vector<float> t(m.frame_floats());
+  for (int i = 0; i < n; ++i) {
+    OP_HIP_CHECK(hipMemcpy(t.data(), m.p + (size_t)(first + i) * m.frame_floats(), t.size() * 4, hipMemcpyDeviceToHost));
+    const int pw = w + 2 * m.pad;
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        const float* px = t.data() + ((size_t)(y + m.pad) * pw + (x + m.pad)) * m.cs;
+        if (pafs)
+          for (int k = 0; k < OP_N_PAF; ++k) pafs[((size_t)i * OP_N_PAF + k) * hw + (size_t)y * w + x] = px[paf_off + k];
+        if (heatmaps)
+          for (int k = 0; k < OP_N_HEAT; ++k)
+            heatmaps[((size_t)i * OP_N_HEAT + k) * hw + (size_t)y * w + x] = px[heat_off + k];
+      }
+  }
+  return OP_OK;
+}
+
 int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double* scores, int32_t cap,
                      op_frame_result* res) {
   using namespace op;
@@ -1688,12 +1964,18 @@ int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double*
   int in_w, in_h, map_w, map_h;
   staged_sizes(c, &in_w, &in_h, &map_w, &map_h);
   int maxp = 0;
+  std::vector<int> big;
   for (int i = 0; i < n; ++i) {
     op_frame_result& r = res[i];
     memset(&r, 0, sizeof(r));
     r.status = hdr[4 * i];
     r.n_peaks = hdr[4 * i + 1];
     r.n_persons = r.status == OP_OK ? hdr[4 * i + 2] : 0;
+    if (r.status == OP_ERR_CAPACITY && c->post_rec.kind) {  // over the batched caps: uncapped re-run
+      big.push_back(i);
+      r.n_persons = 0;
+      r.status = OP_OK;
+    }
     r.map_w = map_w;
     r.map_h = map_h;
     r.net_w = in_w;
@@ -1725,6 +2007,15 @@ int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double*
       const size_t k = (size_t)res[i].n_persons;
       memcpy((char*)poses + (size_t)i * cap * 54 * 8, hp + i * prow, k * 54 * 8);
       memcpy((char*)scores + (size_t)i * cap * 8, hs + i * srow, k * 8);
+    }
+  }
+  for (int i : big) {  // frames over the batched caps, re-run one at a time in big mode
+    op_frame_result& r = res[i];
+    const int rc = read_result(c, first + i, poses + (size_t)i * cap * 54, scores + (size_t)i * cap, cap, &r);
+    if (rc == OP_ERR_HIP || (rc == OP_ERR_CAPACITY && r.n_persons > cap)) return rc;
+    if (rc) {
+      r.status = rc;
+      r.n_persons = 0;
     }
   }
   return OP_OK;
@@ -1761,7 +2052,7 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
 // per scale one batched forward of the n frames (cubic resize + pad + normalise per frame), then
 // per frame the cubic map resizes into its running mean (psum: [frame][38 paf | 19 heat][h][w]),
 // then the full-resolution post-process of all n frames (results at frame index f).
-static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h) {
+static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, bool staged) {
   const int ds = c->prm.downscale;
   const int ns = c->prm.n_scales;
   int rws[OP_MAX_SCALES], rhs[OP_MAX_SCALES], pws[OP_MAX_SCALES], phs[OP_MAX_SCALES];
@@ -1830,13 +2121,24 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h) {
                                         c->stream));
     }
   }
-  // :474-482 post-process at the original resolution: img_len = orig_w, no rescale
+  // :474-482 post-process at the original resolution: img_len = orig_w, no rescale.  With staged
+  // full-resolution maps (op_stage_maps at the frame size + op_use_staged_maps) the post-process
+  // reads those instead of the averaged maps (which are still computed).
+  const float* post_maps = c->d_psum;
+  if (c->use_maps && staged) {
+    if (c->fm_n < n || c->fm_h != h || c->fm_w != w) {
+      set_error("staged full-resolution maps do not match the staged frames (n, h, w)");
+      return OP_ERR_STATE;
+    }
+    post_maps = c->d_fmaps;
+  }
   RC(ensure_post(c, n, h, w));
   PostShape s;
   post_shape(c, s, n, h, w, h, w, (double)w, 1.0, 1.0);
-  const float* sum_heat0 = c->d_psum + (size_t)OP_N_PAF * h * w;
+  post_record(c, 2, nullptr, post_maps, fplanes, s);
+  const float* sum_heat0 = post_maps + (size_t)OP_N_PAF * h * w;
   RC(launch_peaks_from_full(sum_heat0, OP_N_JOINTS, h, w, s, c->pb, c->stream, fplanes));
-  RC(launch_connections_full(c->d_psum, h, w, s, c->pb, c->stream, fplanes));
+  RC(launch_connections_full(post_maps, h, w, s, c->pb, c->stream, fplanes));
   RC(launch_grouping(s, c->pb, c->stream));
   *net_w = pws[ns - 1];
   *net_h = phs[ns - 1];
@@ -1855,9 +2157,16 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
   RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
                                 hipMemcpyHostToDevice, c->stream));
-  c->st_n = 0;  // the staged frame set is replaced
+  // the staged frame set is replaced by this frame (its result stays fetchable as frame 0)
+  c->st_n = 0;
   int net_w = 0, net_h = 0;
-  RC(precise_run(c, 1, h, w, &net_w, &net_h));
+  RC(precise_run(c, 1, h, w, &net_w, &net_h, false));
+  c->st_n = 1;
+  c->st_h = h;
+  c->st_w = w;
+  c->st_precise = true;
+  c->st_net_w = net_w;
+  c->st_net_h = net_h;
   const float* sum_paf = c->d_psum;
   const float* sum_heat = c->d_psum + (size_t)OP_N_PAF * h * w;
   if (pafs_out)
@@ -1882,7 +2191,7 @@ int op_run_staged_precise(op_ctx* c) {
     return OP_ERR_STATE;
   }
   int net_w = 0, net_h = 0;
-  RC(precise_run(c, c->st_n, c->st_h, c->st_w, &net_w, &net_h));
+  RC(precise_run(c, c->st_n, c->st_h, c->st_w, &net_w, &net_h, true));
   c->st_precise = true;
   c->st_net_w = net_w;
   c->st_net_h = net_h;

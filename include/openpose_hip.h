@@ -160,6 +160,14 @@ int op_forward_stages(op_ctx* ctx, const float* x, int32_t n, int32_t h, int32_t
 /* F.resize_images (pose_detector.py:501-502; Chainer <= 6 align-corners bilinear): (c,h,w) -> (c,oh,ow). */
 int op_resize_images(op_ctx* ctx, const float* x, int32_t c, int32_t h, int32_t w, int32_t oh, int32_t ow, float* y);
 
+/* Capacities.  Like the reference (pose_detector.py:75-250 has no caps) the post-process is
+ * uncapped: a frame with more peaks per joint than op_limits.max_peaks_per_joint, or more subsets
+ * than the batched grouping holds, is re-run alone with buffers sized from its own counts (only
+ * device memory bounds it).  OP_ERR_CAPACITY then means either that device memory ran out, or
+ * that the caller's output array is too small -- in which case the needed row count is written
+ * to the count output (*n_peaks, conn_off[19], *n_subsets, res->n_persons) so the call can be
+ * repeated with a larger array. */
+
 /* compute_peaks_from_heatmaps (pose_detector.py:75-110, CPU semantics): heatmaps (c, h, w),
  * channel c-1 dropped.  peaks: rows [joint, x, y, score, id] f64. */
 int op_compute_peaks(op_ctx* ctx, const float* heatmaps, int32_t c, int32_t h, int32_t w,
@@ -185,8 +193,11 @@ int op_postprocess(op_ctx* ctx, const float* paf_low, const float* heat_low, int
 
 /* Copy n BGR frames (n x h x w x 3 u8, contiguous) into the context's HBM staging area. */
 int op_stage_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, int32_t w);
-/* Optional: post-process these network-resolution maps (n x 57 x mh x mw: 38 PAF then 19 heat)
- * instead of the network's own last stage (synthetic-map benchmarking; default off). */
+/* Optional: post-process these maps (n x 57 x mh x mw: 38 PAF then 19 heat) instead of the network's
+ * own (synthetic-map benchmarking; default off; op_use_staged_maps).  mh x mw = the network map size
+ * (h/8 x w/8 of the network input) feeds op_run_staged; mh x mw = the staged frame size (stage the
+ * frames first) feeds op_run_staged_precise's full-resolution post-process in place of the averaged
+ * maps, which are still computed. */
 int op_stage_maps(op_ctx* ctx, const float* maps, int32_t n, int32_t mh, int32_t mw);
 int op_use_staged_maps(op_ctx* ctx, int32_t enable);
 /* Enqueue the full path (resize+normalise, 92 convs, post-process) on the staged frames; async. */
@@ -208,6 +219,12 @@ int op_fetch_result(op_ctx* ctx, int32_t frame, double* poses, double* scores, i
 int op_fetch_results(op_ctx* ctx, int32_t first, int32_t n, double* poses, double* scores, int32_t cap,
                      op_frame_result* res);
 
+/* Network maps of staged frames [first, first+n) after op_synchronize: the last-stage maps of
+ * op_run_staged (pafs (n, 38, h/8, w/8), heatmaps (n, 19, h/8, w/8) of the network input h x w), or
+ * after op_run_staged_precise the averaged full-resolution maps (n, 38|19, H, W) -- the
+ * self.pafs / self.heatmaps detect_precise leaves (pose_detector.py:469-470).  *mh, *mw receive the
+ * map size; pafs = heatmaps = NULL only queries it. */
+int op_fetch_maps(op_ctx* ctx, int32_t first, int32_t n, float* pafs, float* heatmaps, int32_t* mh, int32_t* mw);
 /* HIP-event timing of the last op_run_staged: ms spent in the conv kernels, the post-process kernels
  * and total, recorded on the context stream. */
 int op_last_timing(op_ctx* ctx, double* conv_ms, double* post_ms, double* total_ms);

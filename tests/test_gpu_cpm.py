@@ -110,7 +110,8 @@ def test_cpm_detect_batch_equals_single_calls(cpm):
     c.set_batch_invariant(True)
     try:
         single = [c.detect(im, 0.05, flip_maps=f) for im, f in zip(crops, flips)]
-        _same(c.detect_batch(crops, 0.05, flip_maps=flips), single)
+        for g, e in zip(c.detect_batch(crops, 0.05, flip_maps=flips), single):
+            _same(g, e)
     finally:
         c.set_batch_invariant(False)
 
@@ -126,7 +127,8 @@ def test_cpm_detect_strided_crop_views(cpm):
         _same(c.detect(v, 0.05), c.detect(np.ascontiguousarray(v), 0.05))
     got = c.detect_batch(views, 0.05)
     exp = c.detect_batch([np.ascontiguousarray(v) for v in views], 0.05)
-    _same(got, exp)
+    for g, e in zip(got, exp):
+        _same(g, e)
 
 
 def test_face_and_hand_detector_api():

@@ -125,7 +125,7 @@ def test_forward_368_vs_oracle(precision_ctx, rand_weights):
     _fwd_check(precision_ctx, rand_weights, x)
 
 
-@pytest.mark.parametrize("shape", [(1, 3, 368, 656), (2, 3, 552, 984), (1, 3, 736, 1312)])
+@pytest.mark.parametrize("shape", [(1, 3, 184, 328), (1, 3, 368, 656), (2, 3, 552, 984), (1, 3, 736, 1312)])
 def test_forward_wide_vs_oracle(ctx, rand_weights, shape):
     """The multi-scale path's wide maps (82 / 123 / 164 columns): the 7x7 raster kernel with the
     tight halo pitch and with frame-aligned tiles (conv_big.hip raster_tiling(wide))."""
@@ -227,6 +227,54 @@ def test_staged_batch_matches_single_and_graph(ctx, prec):
             assert np.array_equal(p, single[i][0]) and np.array_equal(s, single[i][1])
     ctx.set_precision("bf16x3")
     ctx.set_batch_invariant(False)
+
+
+def test_graph_replay_follows_batch_invariant_switch(ctx):
+    """A hipGraph captured for one staged frame in the default mode (its small launches split K)
+    is not replayed after op_set_batch_invariant(1): the replay equals the eager batch-invariant
+    run bit for bit, and switching back restores the split-K replay (graph key)."""
+    frame = np.random.default_rng(21).integers(0, 256, (1, 368, 368, 3), dtype=np.uint8)
+    ctx.stage_frames(frame)
+    ctx.set_batch_invariant(False)
+    ctx.run_staged(graph=True)
+    ctx.synchronize()
+    split_maps = ctx.fetch_maps(0, 1)
+    try:
+        ctx.set_batch_invariant(True)
+        ctx.run_staged(graph=True)
+        ctx.synchronize()
+        g = ctx.fetch_maps(0, 1)
+        ctx.run_staged(graph=False)
+        ctx.synchronize()
+        e = ctx.fetch_maps(0, 1)
+        assert np.array_equal(g[0], e[0]) and np.array_equal(g[1], e[1])
+    finally:
+        ctx.set_batch_invariant(False)
+    ctx.run_staged(graph=True)
+    ctx.synchronize()
+    back = ctx.fetch_maps(0, 1)
+    assert np.array_equal(back[0], split_maps[0]) and np.array_equal(back[1], split_maps[1])
+    # split-K and invariant sums differ only by f32 re-association
+    assert np.abs(split_maps[0] - e[0]).max() <= 1e-4 and np.abs(split_maps[1] - e[1]).max() <= 1e-4
+
+
+def test_fetch_maps_equals_forward_of_preprocessed_frames(ctx):
+    """op_fetch_maps after op_run_staged = op_forward of the op_preprocess'ed frames (the staged
+    path resamples the input inside its first conv kernel)."""
+    frames = np.random.default_rng(22).integers(0, 256, (2, 300, 420, 3), dtype=np.uint8)
+    ctx.set_batch_invariant(True)
+    try:
+        ctx.stage_frames(frames)
+        ctx.run_staged()
+        ctx.synchronize()
+        pafs, heat = ctx.fetch_maps(0, 2)
+        x = np.concatenate([ctx.preprocess(f, 520, 368) for f in frames])  # compute_optimal_size: 520 x 368
+        wp, wh = ctx.forward(x)
+    finally:
+        ctx.set_batch_invariant(False)
+    assert pafs.shape == (2, 38, 46, 65) and heat.shape == (2, 19, 46, 65)
+    err = max(float(np.abs(pafs - wp).max()), float(np.abs(heat - wh).max()))
+    assert err <= 1e-5, err
 
 
 def test_staged_synthetic_maps_match_reference(ctx):
