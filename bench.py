@@ -1,16 +1,22 @@
 """Benchmark of the MI355X OpenPose path: frames/s end-to-end (CNN + PAF grouping) at 368x368.
 
 python bench.py [--gpus N --steps K --warmup W --batch B]
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL gather of the per-frame
-result records to every rank).  A step = one batch of B frames per GPU through the whole path:
-uint8 BGR frame in HBM -> resize + normalise -> 92 convs -> upsample / Gaussian / NMS ->
-line integrals -> greedy assignment -> grouping -> poses copied to the host.
+For N > 1 launch one process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT; nothing here imports PyTorch): frames shard round-robin over the ranks,
+and each step's per-frame result records are gathered to rank 0 by RCCL from device memory
+(frames.RcclGather / gather.hip), overlapped with the next step.
+
+A step = one batch of B frames per GPU through the whole PoseDetector.__call__ path:
+  pinned host frames --(copy stream, overlapped with the previous step)--> HBM ring ->
+  resize + normalise -> 92 convs -> upsample / Gaussian / NMS -> line integrals -> greedy
+  assignment -> grouping -> poses copied to the host (and, N > 1, gathered to rank 0).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for every field.
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -22,8 +28,8 @@ PKG = "chainer_realtime_multi-person_pose_estimation_amd"
 METRIC = "frames/sec end-to-end (CNN+PAF grouping) at 368×368, 1/2/4/8 MI355X"
 FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA peak
-HBM_PEAK_GBS = 8000.0
-PARAMS_SCALES = [0.5, 1, 1.5, 2]  # entity.py:74 inference_scales
+PARAMS_SCALES = [0.5, 1, 1.5, 2]  # entity.py:72 inference_scales
+GATHER_PERSONS = 64  # persons carried per frame record (~28 KB per frame)
 
 
 def precise_net(h, w, scale, size=368, stride=8):
@@ -34,7 +40,7 @@ def precise_net(h, w, scale, size=368, stride=8):
     return rh + (-rh) % stride, rw + (-rw) % stride
 
 
-def synthetic_maps(batch, lh=46, lw=46):
+def golden_maps(lh, lw):
     """COCO-like last-stage maps (38 PAF + 19 heat) from the reference's own label generators
     (tests/golden/*.npz, made by tests/golden/make_golden.py): 6 people at 46x46 (368x368 frames),
     20 people at 46x82 (1280x720 frames); None for other map sizes."""
@@ -42,45 +48,58 @@ def synthetic_maps(batch, lh=46, lw=46):
     if name is None:
         return None
     d = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"))
-    m = np.concatenate([d["paf_low"], d["heat_low"]])[None]
-    return np.ascontiguousarray(np.repeat(m, batch, axis=0))
+    return np.concatenate([d["paf_low"], d["heat_low"]])
 
 
 def optimal_size(h, w, size=368, stride=8):
     """compute_optimal_size (pose_detector.py:57-73): (net_w, net_h)."""
     if w < h:
-        ow = size
-        oh = np.round(size * h / w)
+        ow, oh = size, np.round(size * h / w)
     else:
-        oh = size
-        ow = np.round(size * w / h)
+        oh, ow = size, np.round(size * w / h)
     ow, oh = int(ow), int(oh)
     return ow + (-ow) % stride, oh + (-oh) % stride
 
 
-def cpu_baseline(frames, maps, n_frames):
-    """The oracle (NumPy Chainer-CPU forward + C post-process restatement), timed per frame."""
-    from oracle import forward as F
-    from oracle import cvresize, postproc as P
-    import importlib
-    W = importlib.import_module(PKG + ".weights").random_weights(seed=0)
+def blas_info():
     try:
         from threadpoolctl import threadpool_info
-        cores = max([int(i.get("num_threads", 1)) for i in threadpool_info()] + [1])
+        info = threadpool_info()
+        blas = [i for i in info if i.get("user_api") == "blas"]
+        if blas:
+            return blas[0].get("internal_api", "?"), int(blas[0].get("num_threads", 1))
     except Exception:
-        cores = os.cpu_count() or 1
-    x = cvresize.preprocess(cvresize.resize_linear_u8(frames[0], 368, 368))
-    F.cocoposenet_forward(W, x)  # warm-up
-    t0 = time.perf_counter()
-    for i in range(n_frames):
-        f = frames[i % len(frames)]
+        pass
+    return "unknown", os.cpu_count() or 1
+
+
+def cpu_baseline(frames, low_maps, n_frames):
+    """The CPU restatement of the reference path on the host cores: oracle forward (Chainer's CPU
+    conv: im2col + np.tensordot sgemm) + the NumPy/SciPy post-process (oracle/postproc_np.py, the
+    reference's own library calls) on the same COCO-like maps; median per frame of n_frames after
+    one warm-up (BASELINE.md CPU-baseline plan)."""
+    from oracle import forward as F
+    from oracle import cvresize
+    from oracle import postproc_np as PN
+    import importlib
+    W = importlib.import_module(PKG + ".weights").random_weights(seed=0)
+    vendor, threads = blas_info()
+
+    def one(f):
+        t0 = time.perf_counter()
         x = cvresize.preprocess(cvresize.resize_linear_u8(f, 368, 368))
         F.cocoposenet_forward(W, x)
-        P.postprocess(maps[i % len(maps), :38], maps[i % len(maps), 38:], f.shape[0], f.shape[1])
-    dt = time.perf_counter() - t0
-    return {"value": n_frames / dt, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": "%d frames: oracle im2col+sgemm forward (368x368, NumPy BLAS) + C post-process "
-                      "restatement on the same 6-person maps; %.1f s total" % (n_frames, dt)}
+        PN.postprocess(low_maps[:38], low_maps[38:], f.shape[0], f.shape[1])
+        return time.perf_counter() - t0
+
+    one(frames[0])  # warm-up
+    times = [one(frames[(i + 1) % len(frames)]) for i in range(n_frames)]
+    med = statistics.median(times)
+    return {"value": round(1.0 / med, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "median of %d frames after 1 warm-up (%.2f s/frame, %.1f s total): oracle forward "
+                      "(im2col + np.tensordot sgemm, 368x368) + NumPy/SciPy post-process restatement "
+                      "(oracle/postproc_np.py) on the 6-person maps" % (n_frames, med, sum(times)),
+            "blas": vendor, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "nproc": os.cpu_count()}
 
 
 KERNEL_7X7 = {0: "conv_bf16x3<7", 1: "conv7_halo_bf16x3", 2: "conv7_halo_bf16x3", 3: "conv_halo_bf16x3<7",
@@ -92,11 +111,14 @@ MFMA_7X7 = {4: "v_mfma_f32_16x16x32_bf16", 5: "v_mfma_f32_16x16x32_bf16", 6: "v_
 
 def committed_traffic(kernel, batch, precision, halo_mode):
     """HBM bytes per launch (read + write) of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/*_traffic.json, FETCH_SIZE x calibrated pattern factor + WRITE_SIZE, tools/summarize_profile.py) taken
-    on this exact workload; (None, None) when no profile matches."""
+    summary (profiles/**/*_traffic.json, FETCH_SIZE x calibrated pattern factor + WRITE_SIZE,
+    tools/summarize_profile.py) taken on this exact workload; (None, None) when none matches."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")) +
+                   glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic.json")),
+                   key=lambda q: os.path.relpath(q, os.path.join(REPO, "profiles")))
+    for p in paths:
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
@@ -108,8 +130,95 @@ def committed_traffic(kernel, batch, precision, halo_mode):
             continue
         for k, v in d.get("kernels", {}).items():
             if k.replace("op::", "").startswith(kernel):
-                best = (int(v["read_bytes"] + v["write_bytes"]), os.path.basename(p))
+                best = (int(v["read_bytes"] + v["write_bytes"]), os.path.relpath(p, os.path.join(REPO, "profiles")))
     return best if best else (None, None)
+
+
+class Runner(object):
+    """One configuration's step loop on this rank: async uploads from a 2-batch pinned pool, the
+    staged path (single scale or precise), result fetch, N > 1 gather of the previous step."""
+
+    def __init__(self, L, ctx, args, B, FH, FW, rank, world, gather):
+        self.L, self.ctx, self.args, self.B, self.rank, self.world, self.gather = L, ctx, args, B, rank, world, gather
+        rng = np.random.default_rng(1234 + rank)
+        self.pool = [L.PinnedFrames(B, FH, FW) for _ in range(2)]
+        for p in self.pool:
+            p.array[...] = rng.integers(0, 256, (B, FH, FW, 3), dtype=np.uint8)
+        self.k = 0
+        self.persons = 0
+        self.outstanding = 0
+        self.ctx.upload_frames(self.pool[0].array)
+
+    def step(self, collect):
+        a, ctx, B = self.args, self.ctx, self.B
+        if a.precise:
+            ctx.run_staged_precise()
+        else:
+            ctx.run_staged(graph=bool(a.graph))
+        if self.world > 1 and self.gather.device:
+            self.gather.g.submit(0, B, self.k * B * self.world + self.rank, self.world)
+        ctx.upload_frames(self.pool[(self.k + 1) % 2].array)  # next step's frames, overlapped
+        ctx.synchronize()
+        res = ctx.fetch_results(0, B)
+        if collect:
+            self.persons += sum(r[2].n_persons for r in res)
+        if self.world > 1:
+            if not self.gather.device:
+                self.gather.g.submit([(self.k * B * self.world + self.rank + i * self.world, r[2].status,
+                                       r[2].n_peaks, r[0], r[1]) for i, r in enumerate(res)])
+            self.outstanding += 1
+            if self.outstanding == 2:  # collect step k-1's gather (step k's is in flight)
+                self.gather.g.wait()
+                self.outstanding -= 1
+        self.k += 1
+
+    def drain(self):
+        while self.outstanding:
+            self.gather.g.wait()
+            self.outstanding -= 1
+
+    def close(self):
+        for p in self.pool:
+            p.close()
+
+
+class Gather(object):
+    def __init__(self, g, device, label):
+        self.g, self.device, self.label = g, device, label
+
+
+def make_gather(Fr, ctx, transport, world):
+    if world == 1:
+        return Gather(None, False, "single GPU (no gather)")
+    try:
+        return Gather(Fr.RcclGather(ctx, transport, GATHER_PERSONS, timeout=300.0), True,
+                      "frame-parallel x%d, RCCL ncclGather of per-frame result records from HBM to rank 0" % world)
+    except Exception as e:  # labelled, never silent: the scaling line says which transport ran
+        return Gather(Fr.HostGather(transport, GATHER_PERSONS), False,
+                      "frame-parallel x%d, TCP gather of result records (RCCL init failed: %s)" % (world, e))
+
+
+def measure(run, ctx, transport, steps, warmup, prof_7x7):
+    for _ in range(warmup):
+        run.step(False)
+    run.drain()
+    ctx.synchronize()
+    ctx.profile_classes(["conv7x7"])
+    ctx.profile(prof_7x7)
+    ctx.profile_reset()
+    if transport:
+        transport.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run.step(True)
+    run.drain()
+    ctx.synchronize()
+    if transport:
+        transport.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    return elapsed, prof
 
 
 def main():
@@ -121,10 +230,11 @@ def main():
                     help="frames per step per GPU (38: the 7x7 kernel's 640-pixel raster tiles, "
                          "ceil(38 x 2116 / 640) = 126 per branch x 2 = 252 workgroups, one per CU)")
     ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
-                    help="post-process input: COCO-like 6-person maps (default) or the random-weight "
+                    help="post-process input: COCO-like multi-person maps (default) or the random-weight "
                          "network's own last stage")
-    ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--cpu-frames", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the network-maps / fp32 side lines")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--graph", type=int, default=0, help="1: replay each step as one captured hipGraph")
     ap.add_argument("--precision", choices=["bf16x3", "fp32"], default="bf16x3",
@@ -140,29 +250,17 @@ def main():
     headline = (FH, FW) == (368, 368) and not args.precise
     if not headline:
         args.no_cpu_baseline = True
+        args.no_variants = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # OP_BENCH_BACKEND=gloo (rehearsal only: N ranks sharing the GPUs of a smaller box, CPU-side
-    # collectives); the product path is RCCL ('nccl'), one rank per GPU
-    backend = os.environ.get("OP_BENCH_BACKEND", "nccl")
-    coll_dev = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            coll_dev = torch.device("cuda", local)
-        else:
-            local = local % max(1, torch.cuda.device_count())
-            dist.init_process_group(backend)
     import importlib
     L = importlib.import_module(PKG + "._lib")
     Wm = importlib.import_module(PKG + ".weights")
     Fr = importlib.import_module(PKG + ".frames")
+    transport = Fr.SocketTransport(rank, world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                                   timeout=300.0) if world > 1 else None
 
     B = args.batch
     net_w, net_h = optimal_size(FH, FW)
@@ -171,88 +269,36 @@ def main():
     limits.max_batch = B
     ctx = L.Context(local, None, limits)
     ctx.set_precision(args.precision)
-    wts = Wm.random_weights(seed=0)
-    if args.precise:
-        # the random network's 1280x720 maps are noise with thousands of spurious peaks per joint
-        # (past the per-frame caps); a -1 bias on the last stage's Mconv7 keeps them below the peak
-        # threshold -- same FLOPs, the post-process still runs its full-resolution passes
-        for k in ("Mconv7_stage6_L1", "Mconv7_stage6_L2"):
-            wts[k] = (wts[k][0], wts[k][1] - np.float32(1.0))
-    ctx.set_weights(wts)
-    rng = np.random.default_rng(1234 + rank)
-    frames = rng.integers(0, 256, (B, FH, FW, 3), dtype=np.uint8)
-    maps = synthetic_maps(B, net_h // 8, net_w // 8)
-    if maps is None or args.precise:
+    ctx.set_weights(Wm.random_weights(seed=0))
+    low = golden_maps(net_h // 8, net_w // 8) if not args.precise else golden_maps(46, 82)
+    if low is None:
         args.maps = "network"
-    ctx.stage_frames(frames)
-    if not args.precise:
-        if args.maps == "synthetic":
-            ctx.stage_maps(maps)
-            ctx.use_staged_maps(True)
-
-    def barrier():
-        if dist is not None:
-            import torch
-            dist.all_reduce(torch.zeros(1, device=coll_dev))
-            if coll_dev is not None:
-                torch.cuda.synchronize()
-
-    persons = 0
-
-    def step(collect):
-        nonlocal persons
-        if args.precise:
-            ctx.run_staged_precise()
-            res = ctx.fetch_results(0, B)
-        else:
-            ctx.run_staged(graph=bool(args.graph))
-            ctx.synchronize()
-            res = ctx.fetch_results(0, B)
-        if collect:
-            persons += sum(r[2].n_persons for r in res)
-        if dist is not None:
-            import torch
-            recs = Fr.pack_records([(rank + world * i, r[2].status, r[2].n_peaks, r[0], r[1])
-                                    for i, r in enumerate(res)], 64)
-            Fr.gather_records(recs, 64, device=coll_dev)
-
-    for _ in range(args.warmup):
-        step(False)
-    ctx.synchronize()
-    # timed region: HIP events only around the dominant kernel (the 7x7 stage convs) for the
-    # roofline, so the per-launch event overhead stays off the other ~90 launches of a step
-    ctx.profile_classes(["conv7x7"])
-    ctx.profile(not args.no_profile and not args.graph)
-    ctx.profile_reset()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    ctx.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = ctx.profile_read()
+    # the post-process input: staged COCO-like maps (the forward still runs in full and writes its
+    # own), at the network map size (__call__) or upsampled to the frame size (detect_precise)
+    ctx.stage_frames(np.zeros((B, FH, FW, 3), np.uint8))
+    if args.maps == "synthetic":
+        m = low if not args.precise else ctx.resize_images(low, FH, FW)
+        ctx.stage_maps(np.ascontiguousarray(np.repeat(m[None], B, axis=0)))
+        ctx.use_staged_maps(True)
+    gather = make_gather(Fr, ctx, transport, world)
+    run = Runner(L, ctx, args, B, FH, FW, rank, world, gather)
+    elapsed, prof = measure(run, ctx, transport, args.steps, args.warmup,
+                            not args.no_profile and not args.graph)
+    persons = run.persons
     # per-class breakdown from a few extra (untimed) steps with every class evented
     ctx.profile_classes(list(ctx.PROFILE_CLASSES))
     ctx.profile(not args.no_profile)
     ctx.profile_reset()
     n_extra = 0 if args.no_profile else 3
     for _ in range(n_extra):
-        if args.precise:
-            step(False)
-        else:
-            ctx.run_staged()
-            ctx.synchronize()
+        run.step(False)
+    run.drain()
+    ctx.synchronize()
     prof_all = ctx.profile_read()
     ctx.profile(False)
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        pt = torch.tensor([float(persons)], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(pt)
-        persons = float(pt.item())
+    if transport:
+        elapsed = transport.all_reduce(elapsed, "max")
+        persons = transport.all_reduce(float(persons), "sum")
 
     frames_total = world * B * args.steps
     value = frames_total / elapsed
@@ -277,23 +323,25 @@ def main():
     stage_ms = {k: round(v[0] / n_extra, 3) for k, v in prof_all.items()} if n_extra else {}
     metric = METRIC if headline else "frames/sec end-to-end (CNN+PAF grouping) at %dx%d%s, 1/2/4/8 MI355X" % (
         FW, FH, " multi-scale (%s)" % "/".join(str(v) for v in PARAMS_SCALES) if args.precise else "")
+    arith = "bf16x3: 3xBF16 split products, f32 accumulate" if args.precision == "bf16x3" else "exact f32 MFMA"
+    maps_desc = ("post-process fed COCO-like %s maps from the reference's label generators%s" % (
+        "6-person" if (FH, FW) == (368, 368) else "20-person",
+        " (upsampled to the frame size: the full-resolution post-process)" if args.precise else "")
+        if args.maps == "synthetic" else "post-process fed the network's own last stage")
     out = {
         "metric": metric, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16x3 (hi/lo split operands, f32 accumulate)" if args.precision == "bf16x3" else "f32",
-        "data": "synthetic: seeded uint8 %dx%d BGR frames %s; random-init CocoPoseNet (He-normal); " % (
-            FW, FH, "resident in HBM (last-stage biases -1: no spurious peaks on the random network's "
-                    "full-resolution maps)" if args.precise else "resident in HBM")
-                + ("post-process fed COCO-like %s network maps (reference label generators)"
-                   % ("6-person" if (FH, FW) == (368, 368) else "20-person") if args.maps == "synthetic"
-                   else "post-process fed the network's own last stage"),
-        "config": {"workload": "%dx%d frames, full PoseDetector.%s path (resize+normalise, 92-conv "
-                               "CocoPoseNet fp32, PAF post-process), batch of %d frames per GPU per step"
-                               % (FW, FH, "detect_precise" if args.precise else "__call__", B),
+        "data": "synthetic: seeded uint8 %dx%d BGR frames from a 2-batch pinned host pool, uploaded every step "
+                "inside the timed region (copy stream, overlapped with the previous step); random-init "
+                "CocoPoseNet (He-normal); %s" % (FW, FH, maps_desc),
+        "config": {"workload": "%dx%d frames, full PoseDetector.%s path (upload, resize+normalise, 92-conv "
+                               "CocoPoseNet in %s, PAF post-process), batch of %d frames per GPU per step"
+                               % (FW, FH, "detect_precise" if args.precise else "__call__", arith, B),
                    "frames_per_step_per_gpu": B, "net_input": "%dx%d" % (net_w, net_h),
                    "heatmap": "%dx%d" % optimal_size(FH, FW, 320) if not args.precise else "%dx%d" % (FW, FH),
-                   "maps": args.maps, "parallelism": "frame-parallel replicas x%d (RCCL gather of results)" % world},
+                   "maps": args.maps, "parallelism": gather.label},
         "persons_per_s": round(persons / elapsed, 2),
         "gflop_per_frame": round((sum(L.forward_flops(*precise_net(FH, FW, sc)) for sc in PARAMS_SCALES)
                                   if args.precise else L.forward_flops(net_h, net_w)) / 1e9, 2),
@@ -301,13 +349,37 @@ def main():
         "stage_ms_note": "HIP-event sums per kernel class over %d untimed profiled steps" % n_extra,
         "roofline": roofline,
     }
+    if not args.no_variants and world == 1:
+        # side lines (not `value`): the same workload with the network's own maps, and in exact f32
+        variants = {}
+        vsteps = 5
+        ctx.use_staged_maps(False)
+        e, _ = measure(run, ctx, None, vsteps, 1, False)
+        variants["maps_network"] = {"value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
+                                    "note": "post-process on the random network's own last-stage maps"}
+        if args.maps == "synthetic":
+            ctx.use_staged_maps(True)
+        ctx.set_precision("fp32")
+        ctx.profile_classes(["conv7x7"])
+        e, p32 = measure(run, ctx, None, vsteps, 1, True)
+        ms, n, fl, _ = p32["conv7x7"]
+        variants["fp32"] = {"value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
+                            "dtype": "f32 (exact f32 MFMA, v_mfma_f32_32x32x2_f32)",
+                            "conv7x7_frac_of_157.3_TFLOPs": round(fl / (ms * 1e-3) / 1e12 / FP32_MATRIX_PEAK_TFLOPS, 4)
+                            if n else None}
+        ctx.set_precision(args.precision)
+        out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(frames, maps, args.cpu_frames)
+        frames = run.pool[0].array[:4].copy()
+        out["cpu_baseline"] = cpu_baseline(frames, low, args.cpu_frames)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    run.close()
+    if gather.g is not None and gather.device:
+        gather.g.close()
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if transport:
+        transport.close()
 
 
 if __name__ == "__main__":

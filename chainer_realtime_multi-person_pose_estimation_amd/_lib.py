@@ -14,7 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libopenpose_hip%s.so" % (
     "." + os.environ["OP_LIB_VARIANT"] if os.environ.get("OP_LIB_VARIANT") else ""))
 
-OP_OK, OP_ERR_INVALID, OP_ERR_HIP, OP_ERR_CAPACITY, OP_ERR_INDEX, OP_ERR_STATE = range(6)
+OP_OK, OP_ERR_INVALID, OP_ERR_HIP, OP_ERR_CAPACITY, OP_ERR_INDEX, OP_ERR_STATE, OP_ERR_TIMEOUT = range(7)
+OP_COMM_ID_BYTES = 128
 N_JOINTS, N_LIMBS, N_PAF, N_HEAT, N_LAYERS = 18, 19, 38, 19, 92
 
 # Every symbol include/openpose_hip.h declares (checked by tests/test_abi.py).
@@ -24,7 +25,9 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
-    "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_detect_precise", "op_resize_cubic",
+    "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_host_alloc", "op_host_free",
+    "op_pack_results", "op_comm_unique_id", "op_comm_create", "op_comm_destroy", "op_comm_gather_results",
+    "op_comm_wait", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
@@ -120,6 +123,15 @@ def lib():
         "op_cpm_peaks": ([P, P, I32, I32, I32, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect": ([P, P, I32, I32, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "op_cpm_detect_batch": ([P, I32, P, P, P, P, ctypes.c_float, P, P, P], ctypes.c_int),
+        "op_pack_results": ([P, I32, I32, I32, ctypes.c_int64, I32, P], ctypes.c_int),
+        "op_comm_unique_id": ([P], ctypes.c_int),
+        "op_comm_create": ([P, I32, I32, P, ctypes.c_double, P], ctypes.c_int),
+        "op_comm_destroy": ([P], ctypes.c_int),
+        "op_comm_gather_results": ([P, P, I32, I32, I32, ctypes.c_int64, I32], ctypes.c_int),
+        "op_comm_wait": ([P, ctypes.c_double, P, P, P], ctypes.c_int),
+        "op_upload_frames": ([P, P, I32, I32, I32], ctypes.c_int),
+        "op_host_alloc": ([ctypes.c_size_t, P], ctypes.c_int),
+        "op_host_free": ([P], ctypes.c_int),
         "op_fetch_maps": ([P, I32, I32, P, P, P, P], ctypes.c_int),
         "op_cpm_set_batch_invariant": ([P, I32], ctypes.c_int),
         "op_train_create": ([I32, I32, I32, I32, P], ctypes.c_int),
@@ -150,6 +162,8 @@ def check(rc, what=""):
         raise IndexError("list assignment index out of range")
     if rc == OP_ERR_INVALID:
         raise ValueError(msg)
+    if rc == OP_ERR_TIMEOUT:
+        raise TimeoutError(msg)
     raise RuntimeError("%s (status %d)" % (msg, rc))
 
 
@@ -421,6 +435,14 @@ class Context(object):
         n, h, w, c = frames.shape
         check(lib().op_stage_frames(self.h, ptr(frames), n, h, w), "op_stage_frames")
 
+    def upload_frames(self, frames):
+        """Asynchronous staging (op_upload_frames): the next run_staged* uses these frames; keep
+        `frames` (ideally a PinnedFrames array) unchanged until that run is enqueued."""
+        if frames.dtype != np.uint8 or frames.ndim != 4 or frames.shape[3] != 3 or not frames.flags.c_contiguous:
+            raise ValueError("expected contiguous (n, h, w, 3) uint8 frames")
+        n, h, w, _ = frames.shape
+        check(lib().op_upload_frames(self.h, ctypes.c_void_p(frames.ctypes.data), n, h, w), "op_upload_frames")
+
     def stage_maps(self, maps):
         maps = np.ascontiguousarray(maps, dtype=np.float32)
         n, c, h, w = maps.shape
@@ -529,6 +551,31 @@ def _row_strided_u8(img):
     if a.dtype != np.uint8 or a.ndim != 3 or a.strides[2] != 1 or a.strides[1] != 3 or a.strides[0] < a.shape[1] * 3:
         a = np.ascontiguousarray(a, np.uint8)
     return a
+
+
+class PinnedFrames(object):
+    """(n, h, w, 3) uint8 frames in page-locked host memory (op_host_alloc), the source of
+    asynchronous uploads (Context.upload_frames)."""
+
+    def __init__(self, n, h, w):
+        nbytes = int(n) * int(h) * int(w) * 3
+        p = ctypes.c_void_p()
+        check(lib().op_host_alloc(nbytes, ctypes.byref(p)), "op_host_alloc")
+        self._p = p
+        buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+        self.array = np.frombuffer(buf, np.uint8).reshape(int(n), int(h), int(w), 3)
+
+    def close(self):
+        if getattr(self, "_p", None) is not None and self._p.value:
+            self.array = None
+            lib().op_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class CpmContext(object):

@@ -112,6 +112,7 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
 // split-K workspace of a stream (conv_big.hip): floats a capture wanted but could not allocate,
 // grow to that size (outside capture; 0 ok), free on stream destruction
 size_t splitk_ws_capture_short(hipStream_t st);
+
 int splitk_ws_reserve(hipStream_t st);
 void splitk_ws_release(hipStream_t st);
 // co-split halo kernel (conv_halo.hip): tile of tr rows x tc cols per workgroup, nh 1-KiB halo pieces per plane

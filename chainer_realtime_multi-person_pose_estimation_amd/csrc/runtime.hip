@@ -273,6 +273,13 @@ struct op_ctx {
   // staging
   uint8_t* d_frames = nullptr;
   size_t frames_bytes = 0;
+  // async frame uploads (op_upload_frames): a 2-slot device ring filled on copy_stream; the next
+  // run waits for its slot's copy and moves it into d_frames on the compute stream
+  hipStream_t copy_stream = nullptr;
+  uint8_t* d_ring[2] = {nullptr, nullptr};
+  size_t ring_bytes[2] = {0, 0};
+  hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  int ring_next = 0, up_slot = -1, up_n = 0, up_h = 0, up_w = 0;
   int st_n = 0, st_h = 0, st_w = 0;
   bool st_precise = false;     // the staged results come from op_run_staged_precise
   int st_net_w = 0, st_net_h = 0;
@@ -1205,6 +1212,15 @@ int op_destroy(op_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
+  if (c->copy_stream) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamDestroy(c->copy_stream);
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
+    if (c->ev_up[i]) (void)hipEventDestroy(c->ev_up[i]);
+    if (c->ev_free[i]) (void)hipEventDestroy(c->ev_free[i]);
+  }
   if (c->stream) {
     (void)hipStreamSynchronize(c->stream);
     splitk_ws_release(c->stream);
@@ -1731,6 +1747,7 @@ int op_stage_frames(op_ctx* c, const uint8_t* frames, int32_t n, int32_t h, int3
     return OP_ERR_INVALID;
   }
   const size_t bytes = (size_t)n * h * w * 3;
+  c->up_slot = -1;  // a pending op_upload_frames is replaced
   RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpyAsync(c->d_frames, frames, bytes, hipMemcpyHostToDevice, c->stream));
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -1786,9 +1803,87 @@ int op_use_staged_maps(op_ctx* c, int32_t enable) {
   return OP_OK;
 }
 
+// A pending op_upload_frames becomes the staged frame set: the compute stream waits for its copy
+// and moves the ring slot into d_frames (the buffer kernels and captured graphs read).
+static int take_upload(op_ctx* c) {
+  if (c->up_slot < 0) return OP_OK;
+  const int k = c->up_slot;
+  c->up_slot = -1;
+  const size_t bytes = (size_t)c->up_n * c->up_h * c->up_w * 3;
+  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
+  OP_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_up[k], 0));
+  OP_HIP_CHECK(hipMemcpyAsync(c->d_frames, c->d_ring[k], bytes, hipMemcpyDeviceToDevice, c->stream));
+  OP_HIP_CHECK(hipEventRecord(c->ev_free[k], c->stream));
+  if (c->st_n != c->up_n || c->st_h != c->up_h || c->st_w != c->up_w) {
+    if (c->gexec) {
+      OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      hipGraphExecDestroy(c->gexec);
+      c->gexec = nullptr;
+    }
+  }
+  c->st_n = c->up_n;
+  c->st_h = c->up_h;
+  c->st_w = c->up_w;
+  return OP_OK;
+}
+
+int op_upload_frames(op_ctx* c, const uint8_t* frames, int32_t n, int32_t h, int32_t w) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!frames || n < 1 || h < 8 || w < 8) {
+    set_error("op_upload_frames: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  if (!c->copy_stream) {
+    OP_HIP_CHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_up[i], hipEventDisableTiming));
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_free[i], hipEventDisableTiming));
+    }
+  }
+  RC(take_upload(c));  // an upload never run is still staged: this one replaces it afterwards
+  const int k = c->ring_next;
+  const size_t bytes = (size_t)n * h * w * 3;
+  if (bytes > c->ring_bytes[k]) {
+    OP_HIP_CHECK(hipStreamSynchronize(c->copy_stream));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    if (c->d_ring[k]) OP_HIP_CHECK(hipFree(c->d_ring[k]));
+    c->d_ring[k] = nullptr;
+    OP_HIP_CHECK(hipMalloc((void**)&c->d_ring[k], bytes));
+    c->ring_bytes[k] = bytes;
+  }
+  // the slot's previous frames must have been moved out by the compute stream first
+  OP_HIP_CHECK(hipStreamWaitEvent(c->copy_stream, c->ev_free[k], 0));
+  OP_HIP_CHECK(hipMemcpyAsync(c->d_ring[k], frames, bytes, hipMemcpyHostToDevice, c->copy_stream));
+  OP_HIP_CHECK(hipEventRecord(c->ev_up[k], c->copy_stream));
+  c->up_slot = k;
+  c->up_n = n;
+  c->up_h = h;
+  c->up_w = w;
+  c->ring_next = k ^ 1;
+  return OP_OK;
+}
+
+int op_host_alloc(size_t bytes, void** p) {
+  if (!p || bytes == 0) return OP_ERR_INVALID;
+  *p = nullptr;
+  if (hipHostMalloc(p, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    op::set_error("hipHostMalloc failed");
+    return OP_ERR_HIP;
+  }
+  return OP_OK;
+}
+
+int op_host_free(void* p) {
+  if (p && hipHostFree(p) != hipSuccess) return OP_ERR_HIP;
+  return OP_OK;
+}
+
 int op_run_staged(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, true));
+  RC(take_upload(c));
   if (c->st_n < 1) {
     set_error("no staged frames");
     return OP_ERR_STATE;
@@ -1799,6 +1894,7 @@ int op_run_staged(op_ctx* c) {
 int op_run_staged_graph(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, true));
+  RC(take_upload(c));
   if (c->st_n < 1) {
     set_error("no staged frames");
     return OP_ERR_STATE;
@@ -1951,6 +2047,69 @@ int op_fetch_maps(op_ctx* c, int32_t first, int32_t n, float* pafs, float* heatm
   return OP_OK;
 }
 
+// ---- fixed-size per-frame result records (the multi-GPU gather's payload, gather.hip) ----
+// Record of frame i: int32 {status, n_peaks, n_persons, 0}, int64 global frame id, 8 pad bytes,
+// then max_persons x 54 f64 poses and max_persons f64 scores (rows past n_persons zero).
+__global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, int max_persons, int64_t frame_base,
+                                                    int frame_stride, char* __restrict__ out, int64_t rec_bytes) {
+  const int i = blockIdx.x;
+  const int f = first + i;
+  char* r = out + (int64_t)i * rec_bytes;
+  const int status = b.res_hdr[4 * f];
+  const int persons = status == OP_OK ? b.res_hdr[4 * f + 2] : 0;
+  const int k = persons < max_persons ? persons : max_persons;
+  if (threadIdx.x == 0) {
+    int32_t* h = (int32_t*)r;
+    h[0] = status;
+    h[1] = b.res_hdr[4 * f + 1];
+    h[2] = persons;
+    h[3] = 0;
+    *(int64_t*)(r + 16) = frame_base + (int64_t)i * frame_stride;
+    *(int64_t*)(r + 24) = 0;
+  }
+  double* poses = (double*)(r + 32);
+  double* scores = poses + (int64_t)max_persons * 54;
+  const double* src = b.res_poses + (int64_t)f * b.maxs * 54;
+  for (int e = threadIdx.x; e < max_persons * 54; e += 256) poses[e] = e < k * 54 ? src[e] : 0.0;
+  for (int e = threadIdx.x; e < max_persons; e += 256) scores[e] = e < k ? b.res_scores[(int64_t)f * b.maxs + e] : 0.0;
+}
+
+int64_t record_bytes(int max_persons) { return 32 + (int64_t)max_persons * 55 * 8; }
+
+// Enqueue the records of staged frames [first, first+n) into dst (device) on the context stream.
+int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame_base, int frame_stride, void* dst,
+                     hipStream_t* stream) {
+  if (first < 0 || n < 1 || first + n > c->st_n || first + n > c->pn || max_persons < 0) {
+    set_error("pack records: bad frame range");
+    return OP_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
+                     frame_stride, (char*)dst, record_bytes(max_persons));
+  OP_AFTER_LAUNCH("pack_records", c->stream);
+  OP_HIP_CHECK(hipGetLastError());
+  *stream = c->stream;
+  return OP_OK;
+}
+
+int ctx_device(op_ctx* c) { return c->device; }
+
+int op_pack_results(op_ctx* c, int32_t first, int32_t n, int32_t max_persons, int64_t frame_base, int32_t frame_stride,
+                    void* host_records) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!host_records) {
+    set_error("op_pack_results: null output");
+    return OP_ERR_INVALID;
+  }
+  const size_t bytes = (size_t)n * record_bytes(max_persons);
+  RC(ensure_scratch(c, bytes));
+  hipStream_t st;
+  RC(ctx_pack_records(c, first, n, max_persons, frame_base, frame_stride, c->d_scratch, &st));
+  OP_HIP_CHECK(hipMemcpyAsync(host_records, c->d_scratch, bytes, hipMemcpyDeviceToHost, st));
+  OP_HIP_CHECK(hipStreamSynchronize(st));
+  return OP_OK;
+}
+
 int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double* scores, int32_t cap,
                      op_frame_result* res) {
   using namespace op;
@@ -2030,6 +2189,7 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
     return OP_ERR_INVALID;
   }
   const size_t bytes = (size_t)h * w * 3;
+  c->up_slot = -1;  // a pending op_upload_frames is replaced
   RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
                                 hipMemcpyHostToDevice, c->stream));
@@ -2154,6 +2314,7 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
     return OP_ERR_INVALID;
   }
   const size_t bytes = (size_t)h * w * 3;
+  c->up_slot = -1;  // a pending op_upload_frames is replaced
   RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
   OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
                                 hipMemcpyHostToDevice, c->stream));
@@ -2186,6 +2347,7 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
 int op_run_staged_precise(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, true));
+  RC(take_upload(c));
   if (c->st_n < 1 || c->st_h < 11 || c->st_w < 11 || c->prm.n_scales < 1) {
     set_error("op_run_staged_precise: no staged frames (>= 11 x 11) or no inference scale");
     return OP_ERR_STATE;

@@ -27,6 +27,7 @@ extern "C" {
 #define OP_ERR_CAPACITY 3 /* a per-frame cap (peaks/persons) was exceeded */
 #define OP_ERR_INDEX 4    /* reference raises IndexError (pose_detector.py:197): a connection hit >=3 subsets */
 #define OP_ERR_STATE 5    /* weights not set / no staged frames */
+#define OP_ERR_TIMEOUT 6  /* a multi-GPU gather did not complete in time (a rank stalled or died) */
 
 #define OP_N_JOINTS 18 /* JointType, entity.py:9-46 */
 #define OP_N_LIMBS 19  /* params['limbs_point'], entity.py:85-105 */
@@ -193,6 +194,16 @@ int op_postprocess(op_ctx* ctx, const float* paf_low, const float* heat_low, int
 
 /* Copy n BGR frames (n x h x w x 3 u8, contiguous) into the context's HBM staging area. */
 int op_stage_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, int32_t w);
+/* Asynchronous staging for a frame stream: copy n BGR frames (n x h x w x 3 u8, contiguous;
+ * page-locked memory from op_host_alloc makes the copy truly asynchronous) on the context's copy
+ * stream into a 2-slot device ring and return.  The next op_run_staged* waits for that copy on the
+ * compute stream and makes these frames the staged set, so the upload of step k+1 overlaps the
+ * compute of step k (the reference uploads each frame inside __call__, pose_detector.py:496-497).
+ * The host buffer must stay untouched until that run has been enqueued. */
+int op_upload_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, int32_t w);
+/* Page-locked host memory for op_upload_frames sources. */
+int op_host_alloc(size_t bytes, void** p);
+int op_host_free(void* p);
 /* Optional: post-process these maps (n x 57 x mh x mw: 38 PAF then 19 heat) instead of the network's
  * own (synthetic-map benchmarking; default off; op_use_staged_maps).  mh x mw = the network map size
  * (h/8 x w/8 of the network input) feeds op_run_staged; mh x mw = the staged frame size (stage the
@@ -241,6 +252,35 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
 double op_forward_flops(int32_t h, int32_t w);
+
+/* ---- Multi-GPU result gather: frames shard round-robin over one process per GPU; the
+ * only exchange is the per-frame result records, gathered to rank 0 over RCCL from device memory ----
+ *
+ * Record of one frame (record_bytes = 32 + max_persons * 55 * 8): int32 {status, n_peaks,
+ * n_persons, 0}, int64 global frame id (frame_base + i * frame_stride), 8 zero bytes, then
+ * max_persons x 18 x 3 f64 poses and max_persons f64 scores (persons past max_persons are not
+ * carried; n_persons still counts them; rows past n_persons are zero).  A frame over the batched
+ * post-process caps carries status OP_ERR_CAPACITY; its rank fetches it with op_fetch_result. */
+int op_pack_results(op_ctx* ctx, int32_t first, int32_t n, int32_t max_persons, int64_t frame_base,
+                    int32_t frame_stride, void* host_records);
+#define OP_COMM_ID_BYTES 128
+typedef struct op_comm op_comm;
+/* RCCL's unique id (ncclGetUniqueId), made by rank 0 and passed to every rank by the host. */
+int op_comm_unique_id(uint8_t* id);
+/* Communicator of `world` ranks on ctx's device (ncclCommInitRankConfig, non-blocking); gives up with
+ * OP_ERR_TIMEOUT after timeout_s. */
+int op_comm_create(op_ctx* ctx, int32_t world, int32_t rank, const uint8_t* id, double timeout_s, op_comm** out);
+int op_comm_destroy(op_comm* comm);
+/* Enqueue: pack the records of staged frames [first, first+n) after ctx's queued work, then
+ * ncclGather them to rank 0 on the communicator's own stream (and copy them to pinned host memory
+ * there).  Returns at once; at most two gathers outstanding (double-buffered: step k's gather
+ * overlaps step k+1's compute).  Every rank passes the same n and max_persons. */
+int op_comm_gather_results(op_comm* comm, op_ctx* ctx, int32_t first, int32_t n, int32_t max_persons,
+                           int64_t frame_base, int32_t frame_stride);
+/* Wait for the oldest outstanding gather, at most timeout_s (then the communicator is aborted and
+ * OP_ERR_TIMEOUT returned).  Rank 0: *records = n_frames records of rec_bytes each in rank order
+ * (valid until the gather two submits later); other ranks: *records = NULL, *n_frames = 0. */
+int op_comm_wait(op_comm* comm, double timeout_s, const void** records, int32_t* n_frames, int64_t* rec_bytes);
 
 /* ---- Face / hand keypoint detectors: FaceNet / HandNet single-branch CPM nets ----
  * face_detector.py:12-56 (FaceDetector), hand_detector.py:12-66 (HandDetector); the same conv kernels

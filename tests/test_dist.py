@@ -1,14 +1,20 @@
-"""World-size-2 gloo rehearsal of the frame-parallel path (frames.py): round-robin sharding +
-gather of fixed-size result records.  Per-frame compute here is the CPU oracle (test only)."""
+"""Frame-parallel path (frames.py) on the CPU, world size 2 and 3, no PyTorch: round-robin
+sharding, the fixed-size result records, the socket transport's gather / broadcast / barrier /
+max-reduce, and the per-rank timeout (a stalled rank fails the others loudly instead of hanging
+them).  Per-frame compute here is the CPU oracle (test only); the device records + RCCL path is
+tests/test_gpu_gather.py."""
+import multiprocessing as mp
 import os
 import socket
+import sys
+import time
 
 import numpy as np
-import torch.multiprocessing as mp
+import pytest
 
-from conftest import REPO, golden_cases, load_golden
+from conftest import REPO, golden_cases, load_golden, pkg_module
 
-MAXP = 64
+MAXP = 8  # smaller than the 20-person golden: records carry the first MAXP persons
 
 
 def _free_port():
@@ -20,7 +26,6 @@ def _free_port():
 
 
 def _frame_results(ids):
-    import sys
     sys.path.insert(0, REPO)
     from oracle import postproc as P
     cases = [c for c in golden_cases() if c != "noise_crowd"]
@@ -33,40 +38,87 @@ def _frame_results(ids):
     return out
 
 
-def _worker(rank, world, port, n_frames, q):
-    import sys
+def _worker(rank, world, port, n_frames, steps, q):
     sys.path.insert(0, REPO)
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
     from importlib import import_module
     F = import_module("chainer_realtime_multi-person_pose_estimation_amd.frames")
-    mine = F.shard(n_frames, rank, world)
-    local = F.pack_records(_frame_results(mine), MAXP)
-    allr = F.gather_records(local, MAXP)
+    t = F.SocketTransport(rank, world, port=port, timeout=60)
+    g = F.HostGather(t, MAXP)
+    got = []
+    for s in range(steps):  # the bench's pattern: submit step s, collect it at the end of step s+1
+        ids = [s * n_frames + i for i in F.shard(n_frames, rank, world)]
+        g.submit(_frame_results(ids))
+        if s > 0:
+            got.append(g.wait())
+    got.append(g.wait())
+    t.barrier()
+    mx = t.all_reduce(float(rank + 1), "max")
+    sm = t.all_reduce(1.0, "sum")
     if rank == 0:
-        q.put(allr)
-    dist.barrier()
-    dist.destroy_process_group()
+        q.put((got, mx, sm))
+    t.close()
 
 
-def test_gloo_two_ranks_gather_matches_single_process():
-    n_frames = 7
+@pytest.mark.parametrize("world,n_frames", [(2, 7), (3, 8)])
+def test_socket_gather_matches_single_process(world, n_frames):
+    F = pkg_module("frames")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_frames, q)) for r in range(2)]
+    steps = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, steps, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, mx, sm = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    import sys
+    assert mx == world and sm == world
+    for s in range(steps):
+        want = F.unpack_records(F.pack_records(_frame_results(range(s * n_frames, (s + 1) * n_frames)), MAXP), MAXP)
+        assert [r[0] for r in got[s]] == list(range(s * n_frames, (s + 1) * n_frames))
+        for a, b in zip(got[s], want):
+            assert a[:3] == b[:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+
+
+def test_records_round_trip_and_person_cap():
+    F = pkg_module("frames")
+    res = _frame_results(range(5))
+    back = F.unpack_records(F.pack_records(res, MAXP), MAXP)
+    for (fid, st, npk, poses, scores), b in zip(res, back):
+        k = min(len(scores), MAXP)
+        assert b[0] == fid and b[1] == st and b[2] == npk
+        assert np.array_equal(b[3], poses[:k]) and np.array_equal(b[4], scores[:k])
+    assert F.record_bytes(64) == 32 + 64 * 55 * 8
+
+
+def _stalled_worker(rank, port, q):
     sys.path.insert(0, REPO)
     from importlib import import_module
     F = import_module("chainer_realtime_multi-person_pose_estimation_amd.frames")
-    want = F.pack_records(_frame_results(list(range(n_frames))), MAXP)
-    assert got.shape == want.shape
-    assert np.array_equal(got, want)
+    t = F.SocketTransport(rank, 2, port=port, timeout=2.0)
+    if rank == 1:
+        time.sleep(6)  # stalls: never joins the gather
+        t.close()
+        return
+    t0 = time.monotonic()
+    try:
+        t.gather(b"x")
+        q.put(("no error", 0.0))
+    except TimeoutError as e:
+        q.put((str(e), time.monotonic() - t0))
+    t.close()
+
+
+def test_gather_times_out_on_a_stalled_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stalled_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msg, dt = q.get(timeout=60)
+    for p in procs:
+        p.join(timeout=30)
+    assert "timed out" in msg and dt < 5.0, (msg, dt)

@@ -1,0 +1,65 @@
+"""The multi-GPU result gather on the device (gather.hip through frames.RcclGather): records packed
+in HBM are byte-identical to frames.pack_records of the fetched results, and RCCL's gather (one
+rank here: RCCL refuses two ranks on one GPU) returns them in order, double buffered."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, pkg_module
+
+pytestmark = pytest.mark.gpu
+MAXP = 4  # fewer than the six golden persons: the cap path is exercised
+
+
+def _staged(ctx, n):
+    d = load_golden("six_people")
+    maps = np.concatenate([d["paf_low"], d["heat_low"]])[None].repeat(n, axis=0)
+    ctx.stage_frames(np.zeros((n, int(d["orig_h"]), int(d["orig_w"]), 3), np.uint8))
+    ctx.stage_maps(maps)
+    ctx.use_staged_maps(True)
+
+
+def _host_records(F, ctx, n, base, stride):
+    res = ctx.fetch_results(0, n)
+    return F.pack_records([(base + i * stride, r.status, r.n_peaks, p, s) for i, (p, s, r) in enumerate(res)], MAXP)
+
+
+def test_device_records_equal_host_records(ctx, lib):
+    F = pkg_module("frames")
+    _staged(ctx, 3)
+    try:
+        ctx.run_staged()
+        ctx.synchronize()
+        want = _host_records(F, ctx, 3, 10, 8)
+        got = np.zeros_like(want)
+        lib.check(lib.lib().op_pack_results(ctx.h, 0, 3, MAXP, 10, 8, got.ctypes.data), "op_pack_results")
+        assert np.array_equal(got, want)
+    finally:
+        ctx.use_staged_maps(False)
+
+
+def test_rccl_gather_one_rank_double_buffered(ctx):
+    F = pkg_module("frames")
+    t = F.SocketTransport(0, 1)
+    g = F.RcclGather(ctx, t, max_persons=MAXP, timeout=30)
+    _staged(ctx, 2)
+    try:
+        ctx.run_staged()
+        g.submit(0, 2, 0, 1)           # step 0's gather (async, behind step 0's post-process)
+        ctx.synchronize()
+        want0 = F.unpack_records(_host_records(F, ctx, 2, 0, 1), MAXP)
+        ctx.run_staged(graph=True)     # step 1 overlaps step 0's gather
+        g.submit(0, 2, 2, 1)
+        got0 = g.wait()
+        ctx.synchronize()
+        want1 = F.unpack_records(_host_records(F, ctx, 2, 2, 1), MAXP)
+        got1 = g.wait()
+        for got, want in ((got0, want0), (got1, want1)):
+            assert [r[0] for r in got] == [r[0] for r in want]
+            for a, b in zip(got, want):
+                assert a[1:3] == b[1:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+        assert got0[0][2] > 0 and len(got0[0][4]) == MAXP
+        with pytest.raises(RuntimeError):
+            g.wait()  # nothing outstanding
+    finally:
+        ctx.use_staged_maps(False)
+        g.close()

@@ -277,6 +277,40 @@ def test_fetch_maps_equals_forward_of_preprocessed_frames(ctx):
     assert err <= 1e-5, err
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_async_uploads_equal_staged_frames(ctx, lib, graph):
+    """op_upload_frames (pinned host -> 2-slot device ring on the copy stream, overlapped with the
+    previous run) gives each run exactly the maps and results of op_stage_frames of the same frames,
+    over alternating ring slots and a shape change."""
+    rng = np.random.default_rng(23)
+    batches = [rng.integers(0, 256, (2, 240, 320, 3), dtype=np.uint8) for _ in range(3)]
+    batches.append(rng.integers(0, 256, (3, 200, 256, 3), dtype=np.uint8))
+    want = []
+    for b in batches:
+        ctx.stage_frames(b)
+        ctx.run_staged(graph=graph)
+        ctx.synchronize()
+        want.append((ctx.fetch_maps(0, len(b)), ctx.fetch_results(0, len(b))))
+    pinned = [lib.PinnedFrames(*b.shape[:3]) for b in batches]
+    for p, b in zip(pinned, batches):
+        p.array[...] = b
+    try:
+        ctx.upload_frames(pinned[0].array)
+        for k in range(len(batches)):
+            ctx.run_staged(graph=graph)
+            if k + 1 < len(batches):
+                ctx.upload_frames(pinned[k + 1].array)  # overlaps run k
+            ctx.synchronize()
+            maps, res = ctx.fetch_maps(0, len(batches[k])), ctx.fetch_results(0, len(batches[k]))
+            (wm, wr) = want[k]
+            assert np.array_equal(maps[0], wm[0]) and np.array_equal(maps[1], wm[1]), k
+            for (p, sc, r), (wp, ws, wr_) in zip(res, wr):
+                assert r.n_peaks == wr_.n_peaks and np.array_equal(p, wp) and np.array_equal(sc, ws)
+    finally:
+        for p in pinned:
+            p.close()
+
+
 def test_staged_synthetic_maps_match_reference(ctx):
     d = load_golden("six_people")
     maps = np.concatenate([d["paf_low"], d["heat_low"]])[None].repeat(2, axis=0)

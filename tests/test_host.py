@@ -70,6 +70,7 @@ def test_frame_sharding_and_records():
     assert all_ids == list(range(13))
     poses = np.arange(2 * 18 * 3, dtype=np.float64).reshape(2, 18, 3)
     rec = F.pack_records([(7, 0, 30, poses, np.array([1.5, 2.5])), (8, 0, 0, np.zeros((0, 18, 3)), np.zeros(0))], 4)
-    fid, st, npk, p, s = F.unpack_record(rec[0], 4)
+    back = F.unpack_records(rec, 4)
+    fid, st, npk, p, s = back[0]
     assert (fid, st, npk) == (7, 0, 30) and np.array_equal(p, poses) and np.array_equal(s, [1.5, 2.5])
-    assert F.unpack_record(rec[1], 4)[3].shape == (0, 18, 3)
+    assert back[1][3].shape == (0, 18, 3)
