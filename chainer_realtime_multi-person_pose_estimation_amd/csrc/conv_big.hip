@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
   for (int pb = 0; pb < NPX; ++pb) {
     const int b = pg * NPX + pb;
     const int r = b / TCB, c = (b % TCB) * 16 + l16;
-    const uint32_t q = (r < rows_here && c < cols_here) ? (uint32_t)(r * tl.pitch + c) : 0u;
+    const uint32_t q = (uint32_t)(r * tl.pitch + c);  // masked lanes read their own (unused) halo slot: no bank clash
     if (pb & 1) qp[pb >> 1] |= q << 16;
     else qp[pb >> 1] = q;
   }

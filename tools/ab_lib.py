@@ -16,7 +16,7 @@ for r in range(rounds):
             env = dict(os.environ, OP_LIB_VARIANT="", **dict(kv.split("=", 1) for kv in v.split(",")))
         else:
             env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
-        p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--steps", "10",
+        p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--no-variants", "--steps", "10",
                             "--warmup", "2"], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode:
             print(p.stdout[-2000:], p.stderr[-2000:])

@@ -11,5 +11,5 @@ for f in $SRC/*.hip; do
   b=$(basename $f .hip); /opt/rocm/bin/hipcc $FLAGS -c $f -o $OUT/$b.o & objs="$objs $OUT/$b.o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $SRC/../libopenpose_hip.$NAME.so $objs
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $SRC/../libopenpose_hip.$NAME.so $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built $SRC/../libopenpose_hip.$NAME.so
