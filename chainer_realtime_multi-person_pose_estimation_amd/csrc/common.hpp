@@ -124,10 +124,6 @@ int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // 3x3 conv + ReLU + 2x2 max-pool fused (conv_big.hip)
 int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
-// 3x3 / 7x7 with double-buffered 8-channel halos (conv_db.hip); pool: fused 2x2 max-pool
-int launch_conv_db(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, bool pool, int* taken);
-// 7x7 tap-pair kernel on v_mfma_f32_16x16x32_bf16 (conv_pair.hip)
-int launch_conv_pair(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // fused 1x1 pair at the end of a branch (conv_head.hip): in -> W1 (ReLU) -> W2 (no ReLU) -> out
 struct HeadGroup {
   const float* in;       // split NHWC input, offset by the group's first input channel

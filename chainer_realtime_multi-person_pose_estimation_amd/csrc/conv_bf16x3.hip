@@ -206,8 +206,6 @@ static int launch_bf16x3_t(const SplitConvShape& s, const SplitConvGroup* g, hip
   return OP_OK;
 }
 
-int launch_conv7_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
-
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st) {
   if (s.c16 <= 0 || (s.ks != 1 && s.ks != 3 && s.ks != 7) || s.pin < s.ks / 2 || s.cs_in % 16 || s.cs_out % 8) {
     set_error("launch_conv_bf16x3: unsupported shape");
@@ -221,29 +219,17 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     }
     if (g[i].cop % 128) wide = false;
   }
-  if (s.halo_mode == 7) {  // double-buffered 8-channel halos (conv_db.hip), 1x1 as mode 4
-    int taken = 0;
-    const int rc = launch_conv_db(s, g, st, false, &taken);
-    if (rc || taken) return rc;
-  }
-  if (s.halo_mode == 6 && s.ks == 7) {  // 16x16x32 tap pairs (conv_pair.hip), then as mode 4
-    int taken = 0;
-    const int rc = launch_conv_pair(s, g, st, &taken);
-    if (rc || taken) return rc;
-  }
-  if (s.halo_mode == 4 || s.halo_mode == 6 || s.halo_mode == 8 || s.halo_mode == 9 || s.halo_mode == 10 || s.halo_mode == 11 || s.halo_mode == 12 || (s.halo_mode == 5 && s.ks == 7)) {  // conv_big.hip
+  // conv algo 4 (default): the shared-weight halo kernels (conv_big.hip), then the co-split halo
+  // kernel for the shapes they leave (the 1x1 convs, narrow maps); algo 3: the co-split halo
+  // kernel first; algo 0 / anything neither takes: the per-tap gather kernel below
+  if (s.halo_mode == 4) {
     int taken = 0;
     const int rc = launch_conv_big(s, g, st, &taken);
     if (rc || taken) return rc;
   }
-  if (s.halo_mode == 3 || s.halo_mode == 4 || s.halo_mode >= 6) {  // co-split halo kernel (conv_halo.hip)
+  if (s.halo_mode == 3 || s.halo_mode == 4) {
     int taken = 0;
     const int rc = launch_conv_halo(s, g, st, &taken);
-    if (rc || taken) return rc;
-  }
-  if (s.ks == 7 && (s.halo_mode == 1 || s.halo_mode == 2)) {
-    int taken = 0;
-    const int rc = launch_conv7_halo(s, g, st, &taken);
     if (rc || taken) return rc;
   }
   if (wide) {
@@ -258,203 +244,6 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     case 3: return launch_bf16x3_t<3, 2, 2>(s, g, st);
     default: return launch_bf16x3_t<7, 2, 2>(s, g, st);
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// 7x7 stage convs with an LDS halo (the dominant kernel: Mconv1..5 of stages 2-6, 68 % of FLOPs).
-//
-// Workgroup tile = CB*32 output channels x up to 256 consecutive pixels of ONE frame (4 waves x
-// 2 blocks of 32).  For each 16-channel chunk the workgroup stages the tile's input rows plus the
-// 3-pixel halo -- a contiguous run of padded rows of the stacked NHWC buffer -- into LDS once, and
-// all 49 taps read their shifted windows from it (reuse ~19x instead of a per-tap gather).  The
-// halo is stored as 4 planes (hi/lo x k-half) of 16 B per pixel (wave w copies plane w), so a
-// wave's B-operand reads are consecutive 16-B slots: conflict-free.  Weights stream through a
-// 3-deep ring of (tap, chunk) tiles; the next chunk's halo is copied into the second buffer
-// during the current chunk.  Every copy is global_load_lds; per step one counted vmcnt + one
-// raw s_barrier.  vmcnt accounting (per wave, issue order): step it issues W(it+2) then, on tap
-// 0, the halo of the next chunk (NH pieces), so W(it) has NW ops after it, plus NH when
-// tap(it) is 1 or 2.
-template <int CB, int NH, bool DH>
-__global__ __launch_bounds__(256, DH ? 1 : 2) void conv7_halo_bf16x3(SplitConvShape s, SplitConvGroup g0,
-                                                                      SplitConvGroup g1, int tiles_per_frame) {
-  constexpr int KS = 7, KSQ = 49, R = 3, PB = 2;
-  constexpr int W_BYTES = CB * 32 * 64;
-  constexpr int NW = W_BYTES / 4096;
-  constexpr int HALO_PLANE = NH * 1024;
-  constexpr int HALO_BYTES = 4 * HALO_PLANE;
-  constexpr int NHB = DH ? 2 : 1;  // halo buffers
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo NHB][W ring 3]
-
-  const SplitConvGroup g = blockIdx.z == 0 ? g0 : g1;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int co_base = blockIdx.y * (CB * 32);
-  if (co_base >= g.cop) return;
-  const int hw = s.h * s.w;
-  const int total = s.n * hw;
-  const int frame = blockIdx.x / tiles_per_frame;
-  const int tile_px0 = (blockIdx.x - frame * tiles_per_frame) * 256;  // within the frame
-  const int wp = s.w + 2 * R;
-  const int hp = s.h + 2 * R;
-  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
-  // halo = padded rows [y_first, y_last + 6] of this frame (padded-row coordinates)
-  const int y_first = tile_px0 / s.w;
-  int last_px = tile_px0 + 255;
-  if (last_px >= hw) last_px = hw - 1;
-  const int y_last = last_px / s.w;
-  const int hrows = y_last - y_first + KS;
-  const int npix = hrows * wp;  // <= NH * 64 by construction (host check)
-  const char* hsrc0 = (const char*)g.in + ((int64_t)(frame * hp + y_first) * wp) * pix_bytes + wave * 16;
-
-  // weight pieces: piece k = wave*NW + j -> plane k / (CB/2), 64-channel half k % (CB/2)
-  const char* wsrc[NW];
-#pragma unroll
-  for (int j = 0; j < NW; ++j) {
-    const int k = wave * NW + j;
-    wsrc[j] = (const char*)g.w + ((int64_t)(k / (CB / 2)) * g.cop + co_base + (k % (CB / 2)) * 64 + lane) * 16;
-  }
-  const int64_t wstep = (int64_t)g.cop * 64;
-  const int n_it = s.c16 * KSQ;
-
-  // this lane's output pixels -> halo pixel index of tap (0,0)
-  const int l32 = lane & 31, hi = lane >> 5;
-  int q0[PB];
-  const int px_base = frame * hw + tile_px0 + wave * (PB * 32);
-#pragma unroll
-  for (int pb = 0; pb < PB; ++pb) {
-    int pf = tile_px0 + wave * (PB * 32) + pb * 32 + l32;  // within the frame
-    if (pf >= hw) pf = hw - 1;
-    const int y = pf / s.w, x = pf - (pf / s.w) * s.w;
-    q0[pb] = (y - y_first) * wp + x;
-  }
-
-  auto stage_w = [&](int it) {
-    char* base = lds + NHB * HALO_BYTES + (it % 3) * W_BYTES;  // slot of the unclamped step: never read again
-    if (it >= n_it) it = n_it - 1;  // keep the per-step op count uniform (the copy is never consumed)
-#pragma unroll
-    for (int j = 0; j < NW; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(wsrc[j] + (int64_t)it * wstep), LDS_PTR(base + (wave * NW + j) * 1024),
-                                       16, 0, 0);
-  };
-  auto stage_halo = [&](int c) {
-    char* base = lds + (DH ? (c & 1) : 0) * HALO_BYTES + wave * HALO_PLANE;  // buffer of the unclamped chunk
-    if (c >= s.c16) c = s.c16 - 1;  // uniform op count; that copy is never read
-#pragma unroll
-    for (int i = 0; i < NH; ++i) {
-      int q = i * 64 + lane;
-      if (q >= npix) q = npix - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(hsrc0 + (int64_t)q * pix_bytes + c * 64), LDS_PTR(base + i * 1024),
-                                       16, 0, 0);
-    }
-  };
-
-  floatx16 acc[CB][PB];
-#pragma unroll
-  for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[cb][pb][r] = 0.0f;
-
-  if (DH) stage_halo(0);
-  stage_w(0);
-  stage_w(1);
-  int c = 0, t = 0;
-  for (int it = 0; it < n_it; ++it) {
-    if (DH && (t == 1 || t == 2))
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW + NH) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (!DH && t == 0) {
-      // single halo buffer: everyone finished the previous chunk (barrier above); load this chunk's
-      // halo, wait for it (W(it+1) is waited for too), and publish it with a second barrier
-      stage_halo(c);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    stage_w(it + 2);
-    if (DH && t == 0) stage_halo(c + 1);
-    const char* wb = lds + NHB * HALO_BYTES + (it % 3) * W_BYTES;
-    const char* hb = lds + (DH ? (c & 1) : 0) * HALO_BYTES;
-    const int ky = t / KS, kx = t - (t / KS) * KS;
-    const int toff = ky * wp + kx;
-    bf16x8 ah[CB], al[CB], bh[PB], bl[PB];
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb) {
-      const char* b = hb + (q0[pb] + toff) * 16;
-      bh[pb] = *(const bf16x8*)(b + (2 * hi) * HALO_PLANE);
-      bl[pb] = *(const bf16x8*)(b + (2 * hi + 1) * HALO_PLANE);
-    }
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      const char* a = wb + (2 * hi) * (CB * 512) + (cb * 32 + l32) * 16;
-      ah[cb] = *(const bf16x8*)a;
-      al[cb] = *(const bf16x8*)(a + CB * 512);
-    }
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) {
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[pb], acc[cb][pb], 0, 0, 0);
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[pb], acc[cb][pb], 0, 0, 0);
-        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[pb], acc[cb][pb], 0, 0, 0);
-      }
-    if (++t == KSQ) {
-      t = 0;
-      ++c;
-    }
-  }
-  // pixels past the end of this frame are masked by the tile bound
-  const int frame_end = frame * hw + hw;
-  store_tile<CB, PB>(s, g, acc, co_base, px_base, frame_end < total ? frame_end : total, hw, lane);
-}
-
-// Halo pieces per wave needed for a 256-pixel tile at width w (7x7, pad 3).
-static int halo_pieces(int w) {
-  const int rows = (255 + w - 1) / w + 1 + 6;  // rows spanned by 256 consecutive pixels + halo
-  return (rows * (w + 6) + 63) / 64;
-}
-
-template <int CB, int NH, bool DH>
-static int launch_halo_t(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st) {
-  const int hw = s.h * s.w;
-  const int tpf = (hw + 255) / 256;
-  const int cop_max = s.groups > 1 ? (g[0].cop > g[1].cop ? g[0].cop : g[1].cop) : g[0].cop;
-  const size_t lds = (DH ? 2 : 1) * 4 * NH * 1024 + 3 * CB * 32 * 64;
-  static bool attr_set = false;
-  if (!attr_set) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv7_halo_bf16x3<CB, NH, DH>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr_set = true;
-  }
-  dim3 grid((unsigned)(s.n * tpf), (unsigned)((cop_max + CB * 32 - 1) / (CB * 32)), (unsigned)s.groups);
-  hipLaunchKernelGGL((conv7_halo_bf16x3<CB, NH, DH>), grid, dim3(256), lds, st, s, g[0], s.groups > 1 ? g[1] : g[0],
-                     tpf);
-  OP_AFTER_LAUNCH("conv7_halo_bf16x3<CB", st);
-  OP_HIP_CHECK(hipGetLastError());
-  return OP_OK;
-}
-
-// Returns 1 if the halo kernel took the launch, 0 if the shape needs the generic kernel.
-int launch_conv7_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
-  *taken = 0;
-  if (s.ks != 7 || s.pin != 3 || s.cs_in % 16) return OP_OK;
-  for (int i = 0; i < s.groups; ++i)
-    if (g[i].cop % 128 || g[i].cin_off % 16) return OP_OK;
-  const int nh = halo_pieces(s.w);
-  *taken = 1;
-  if (s.halo_mode == 2) {  // double-buffered halo, 1 workgroup per CU
-    if (nh <= 12) return launch_halo_t<4, 12, true>(s, g, st);
-    if (nh <= 16) return launch_halo_t<4, 16, true>(s, g, st);
-  } else {  // single halo buffer, 2 workgroups per CU
-    if (nh <= 12) return launch_halo_t<4, 12, false>(s, g, st);
-    if (nh <= 16) return launch_halo_t<4, 16, false>(s, g, st);
-  }
-  *taken = 0;
-  return OP_OK;
 }
 
 // ---- split-format helpers ----

@@ -9,10 +9,6 @@
 //    as 4 planes (hi/lo x k-half) of 16 B per pixel and all KSxKS taps read their shifted window
 //    from there.  The LDS row pitch is TC + 16 slots when a 32-pixel block wraps a tile row (every
 //    ds_read_b128 lane group stays on distinct banks), the tight TC + KS - 1 when TC % 32 == 0.
-//  * DB (conv algo 8, 3x3 c128): two halo buffers; the next chunk's halo streams in, a few pieces
-//    per tap, while this chunk's taps run (2 x 4-wave workgroups per CU at 80 KiB each).  Parity-
-//    tested but ~2 % slower on the 3x3 layers than the default in an interleaved in-process A/B
-//    (tools/ab_algo.py): the reload latency is already covered by the co-resident workgroup.
 //  * Weights: (tap, chunk) tiles of CW channels x 4 planes stream through an LDS ring by
 //    global_load_lds (each wave copies its pieces), one counted vmcnt + one s_barrier per tap
 //    (PAIR = 0, 3-deep ring) or per pair of taps (PAIR = 1, 6-deep ring, 4 taps ahead; raster
@@ -38,14 +34,6 @@ typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4g __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR_G(p) ((__attribute__((address_space(3))) void*)(p))
-
-// cache policy of the conv_m16 / conv_m16k halo loads (timing experiments; 0 = default)
-#ifndef M16_HALO_AUX
-#define M16_HALO_AUX 0
-#endif
-#ifndef M16K_HALO_AUX
-#define M16K_HALO_AUX 0
-#endif
 
 struct BigTiling {
   int32_t tr, tc;            // tile rows x cols
@@ -130,46 +118,7 @@ __device__ __forceinline__ void big_taps(int nt, floatx16 (&acc)[2][NPB], const 
   }
 }
 
-// One tap for one wave with the A fragments already in registers (WREG): 2 channel blocks x NPB
-// pixel blocks; bh/bl[0] hold block 0 of this tap on entry and, when `next`, block 0 of tap t+1
-// on exit (same halo), so no tap starts on an LDS round trip.
-template <int NPB, int KS>
-__device__ __forceinline__ void wv_tap(floatx16 (&acc)[2][NPB], const char* bp0, int hplane,
-                                       const uint32_t (&qp)[(NPB + 1) / 2], const bf16x8g (&ah)[2],
-                                       const bf16x8g (&al)[2], bf16x8g (&bh)[2], bf16x8g (&bl)[2], int t, int pitch,
-                                       bool next) {
-  auto q0 = [&](int pb) -> int { return (int)((qp[pb >> 1] >> (16 * (pb & 1))) & 0xffffu); };
-  const int toff = (t / KS) * pitch + (t - (t / KS) * KS);
-  const int tn = t + 1;
-  const int toff_n = (tn / KS) * pitch + (tn - (tn / KS) * KS);
-#pragma unroll
-  for (int pb = 0; pb < NPB; ++pb) {
-    const int cur = pb & 1;
-    if (pb + 1 < NPB) {
-      bh[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + (q0(pb + 1) + toff) * 16);
-      bl[(pb + 1) & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(pb + 1) + toff) * 16);
-    } else if (next) {
-      bh[NPB & 1] = *(const bf16x8g*)(bp0 + (q0(0) + toff_n) * 16);
-      bl[NPB & 1] = *(const bf16x8g*)(bp0 + hplane + (q0(0) + toff_n) * 16);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
-      acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-    }
-  }
-  if constexpr (NPB & 1) {
-    const bf16x8g th = bh[0], tl = bl[0];
-    bh[0] = bh[1];
-    bl[0] = bl[1];
-    bh[1] = th;
-    bl[1] = tl;
-  }
-}
-
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool DB, bool RASTER, bool WREG>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL, bool RASTER>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                                    SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -179,19 +128,14 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   constexpr int PLANE_W = CW * 16;       // bytes of one weight plane of the tile
   constexpr int SLOT_W = 4 * PLANE_W;    // one (tap, chunk) weight tile
   constexpr int NWP = 4 * CH / NWAVE;    // 1-KiB weight pieces per wave per tap
-  // DB (double-buffered halo, 2 workgroups per CU at <= 80 KiB each) keeps a 2-slot weight ring
   // tap pairs use a 4-slot ring (2 taps ahead) where LDS is tight: RASTER (tiles over the batch's
   // raster order, 2 halo regions) and 3x3 (2 workgroups per CU)
   constexpr bool RING4 = RASTER || KS == 3;
-  // WREG: no weight ring -- every wave loads its own A fragments from L2 straight into registers,
-  // one tap ahead, so the taps need no workgroup barrier at all (only the halo reload does)
-  constexpr int RING = WREG ? 0 : PAIR ? (RING4 ? 4 : 6) : (DB ? 2 : 3);
-  constexpr int AHEAD = PAIR ? (RING4 ? 2 : 4) : (DB ? 1 : 2);  // taps between a weight copy's issue and its use
+  constexpr int RING = PAIR ? (RING4 ? 4 : 6) : 3;
+  constexpr int AHEAD = PAIR ? (RING4 ? 2 : 4) : 2;  // taps between a weight copy's issue and its use
   constexpr int CAP = PG * NPB * 32;     // output pixels per tile
   static_assert(NWP >= 1 && NWP <= 2 && PG >= 1, "wave / channel split");
-  static_assert(!DB || !PAIR, "double-buffered halo runs one tap per barrier");
-  static_assert(!RASTER || (!DB && !POOL), "raster tiles: single halo buffer, plain epilogue");
-  static_assert(!WREG || (!DB && !PAIR), "register weights: one tap at a time, single halo buffer");
+  static_assert(!RASTER || !POOL, "raster tiles: plain epilogue");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
 
   // ---- which tile / weight set ----
@@ -254,7 +198,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     wsrc[i] = (const char*)g.w + (j / CH) * wplane + ((int64_t)co0 + 64 * (j % CH) + lane) * 16;
     wdst[i] = (j / CH) * PLANE_W + (j % CH) * 1024;
   }
-  // split-K (tl.ksplit > 1, non-PF only): this workgroup runs input chunks [cb0, cb1)
+  // split-K (tl.ksplit > 1): this workgroup runs input chunks [cb0, cb1)
   const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
   const int split = nsplit > 1 ? (int)blockIdx.y : 0;
   const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
@@ -298,9 +242,8 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[cb][pb][e] = 0.0f;
 
-  if constexpr (!WREG)
 #pragma unroll
-    for (int i = 0; i < AHEAD; ++i) stage_w(i);
+  for (int i = 0; i < AHEAD; ++i) stage_w(i);
   const char* const bp0 = halo + (2 * hi) * hplane;  // this lane's k-half: hi plane, lo plane follows
   const int wlane = (ch * 64 + l32) * 16;
   constexpr int HSTEP = NWAVE / 4;
@@ -308,86 +251,12 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
   int it = 0;
-  if constexpr (DB) {
-    // ---- double-buffered halo: chunk c+1's halo streams into the other buffer during chunk c,
-    // a few 1-KiB pieces per tap right behind that tap's weight copy (taps 0 .. KSQ-2); the counted
-    // vmcnt of each tap leaves only the previous tap's pieces in flight, so all of them have landed
-    // (and passed a barrier) before chunk c+1's first tap.
-    const int hbytes = 4 * hplane;
-    const int np_w = (tl.nh - h_i0 + HSTEP - 1) / HSTEP;  // pieces of one chunk for this wave
-    const int ppt = (np_w + KSQ - 2) / (KSQ - 1);        // per tap, all issued by tap KSQ-2
-    auto halo_piece = [&](const char* src0, char* dst, int hr, int hc) {
-      const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-      glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
-    };
-    {  // chunk 0, whole
-      int hr = h_r0, hc = h_c0;
-      char* dst = halo + h_plane * hplane + h_i0 * 1024;
-      for (int i = h_i0; i < tl.nh; i += HSTEP) {
-        halo_piece(fbase + h_plane * 16, dst, hr, hc);
-        dst += HSTEP * 1024;
-        hc += HSTEP * 64;
-        while (hc >= tl.pitch) {
-          hc -= tl.pitch;
-          ++hr;
-        }
-      }
-      wait_vmcnt<0>();
-    }
-    for (int c = 0; c < s.c16; ++c) {
-      const bool pf = c + 1 < s.c16;
-      const char* hsrc = fbase + (c + 1) * 64 + h_plane * 16;
-      char* hdst = halo + ((c + 1) & 1) * hbytes + h_plane * hplane + h_i0 * 1024;
-      int hr = h_r0, hc = h_c0, k = 0, n1 = 0;
-      const char* const bp = halo + (c & 1) * hbytes + (2 * hi) * hplane;
-#pragma unroll 1
-      for (int t = 0; t < KSQ; ++t, ++it) {
-        // W(it) (issued one tap back, before that tap's pieces) landed for this wave ...
-        wait_vm_dyn(n1);
-        __builtin_amdgcn_s_barrier();  // ... and for every wave; slot (it+1) % 2 and the other halo are free
-        asm volatile("" ::: "memory");
-        stage_w(it + 1);
-        int n = 0;
-        if (pf)
-          for (; n < ppt && k < np_w; ++n, ++k) {
-            halo_piece(hsrc, hdst, hr, hc);
-            hdst += HSTEP * 1024;
-            hc += HSTEP * 64;
-            while (hc >= tl.pitch) {
-              hc -= tl.pitch;
-              ++hr;
-            }
-          }
-        n1 = n;
-        const char* wb = lds + (it % RING) * SLOT_W + wlane;
-        big_taps<NPB, KS, PLANE_W>(1, acc, bp, hplane, qp, wb, wb, t, tl.pitch, hi);
-      }
-    }
-  } else {
-  bf16x8g wa_h[2], wa_l[2], wn_h[2], wn_l[2], wb_h[2], wb_l[2];
-  const char* const wl = (const char*)g.w + ((int64_t)co0 + ch * 64 + l32) * 16 + (2 * hi) * wplane;
-  auto load_a = [&](int it2, bf16x8g (&ah)[2], bf16x8g (&al)[2]) {  // WREG: this lane's A fragments of step it2
-    if (it2 >= n_it) it2 = n_it - 1;
-    const char* p = wl + (int64_t)it2 * wstep;
-    ah[0] = *(const bf16x8g*)p;
-    ah[1] = *(const bf16x8g*)(p + 512);
-    al[0] = *(const bf16x8g*)(p + wplane);
-    al[1] = *(const bf16x8g*)(p + wplane + 512);
-  };
-  if constexpr (WREG) load_a(0, wa_h, wa_l);
   for (int c = 0; c < s.c16; ++c) {
     // ---- halo reload; everyone is past the previous chunk's reads ----
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-#ifdef BIG_SKIP_RELOAD  // timing experiment only (wrong results): halo loaded for chunk 0 only
-    if (c == 0)
-#endif
     {
-#ifdef BIG_SAME_CHUNK  // timing experiment only (wrong results): every chunk re-reads chunk 0
-      const char* src0 = fbase + h_plane * 16;
-#else
       const char* src0 = fbase + c * 64 + h_plane * 16;
-#endif
       const char* src0_b = fbase_b + c * 64 + h_plane * 16;
       // wave w copies plane w%4, pieces w/4, w/4 + NWAVE/4, ...: the halo slot advances by a
       // fixed stride, so (row, col) are stepped, not divided, per piece
@@ -411,29 +280,14 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr (WREG) {
-      wb_h[0] = *(const bf16x8g*)(bp0 + (int)(qp[0] & 0xffffu) * 16);  // block 0 of tap 0
-      wb_l[0] = *(const bf16x8g*)(bp0 + hplane + (int)(qp[0] & 0xffffu) * 16);
-#pragma unroll 1
-      for (int t = 0; t < KSQ; ++t, ++it) {
-        load_a(it + 1, wn_h, wn_l);  // next step's A: lands during this tap's MFMAs
-        wv_tap<NPB, KS>(acc, bp0, hplane, qp, wa_h, wa_l, wb_h, wb_l, t, tl.pitch, t + 1 < KSQ);
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          wa_h[cb] = wn_h[cb];
-          wa_l[cb] = wn_l[cb];
-        }
-      }
-    } else if constexpr (PAIR) {
+    if constexpr (PAIR) {
 #pragma unroll 1
       for (int t = 0; t < KSQ; t += 2) {
         // taps (t, t+1) share one barrier: W(it), W(it+1) landed for this wave (W(it+2), W(it+3)
         // may be in flight; after a 1-tap tail the count over-waits, which is safe) ...
         wait_vmcnt<AHEAD == 4 ? 2 * NWP : 0>();
         // ... and for every wave; every wave is also done with the slots of the previous pair
-#ifndef BIG_NO_TAP_BARRIER  // timing experiment only (races on the weight ring)
         __builtin_amdgcn_s_barrier();
-#endif
         asm volatile("" ::: "memory");
         stage_w(it + AHEAD);
         stage_w(it + AHEAD + 1);
@@ -446,16 +300,13 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 #pragma unroll 1
       for (int t = 0; t < KSQ; ++t, ++it) {
         wait_vmcnt<NWP>();  // W(it) landed for this wave (W(it+1) may be in flight) ...
-#ifndef BIG_NO_TAP_BARRIER
         __builtin_amdgcn_s_barrier();  // ... and for every wave; slot (it-1) % 3 is free
-#endif
         asm volatile("" ::: "memory");
         stage_w(it + 2);
         const char* wb = lds + (it % RING) * SLOT_W + wlane;
         big_taps<NPB, KS, PLANE_W>(1, acc, bp0, hplane, qp, wb, wb, t, tl.pitch, hi);
       }
     }
-  }
   }
   wait_vmcnt<0>();  // drain the trailing (never read) weight copies
 
@@ -551,15 +402,9 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
           vl[e] = __builtin_bit_cast(unsigned short, l16);
         }
         char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
-#ifdef BIG_NO_STORE  // timing experiment only: epilogue stores skipped unless the value is a NaN
-        if (v[0] != v[0]) {
-#endif
         *(u16x4g*)d = vh;
         *(u16x4g*)(d + 16) = vl;
         if (o32) *(floatx4*)(o32 + co) = v;
-#ifdef BIG_NO_STORE
-        }
-#endif
       }
   }
 }
@@ -573,11 +418,7 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
 // 64 channels (4 blocks of 16) x NPX 16-pixel blocks of a raster tile; D rows are channels (4
 // consecutive per lane), columns pixels.  Halo, 4-slot weight ring (one barrier per tap pair, 2
 // taps ahead) and XCD-aware block order as conv_big_bf16x3<7,..,RASTER>.
-// PF (OP_M16_PF=1): the next tap pair's A fragments and first B fragment are read in the last
-// pixel block of the current pair, each A register right after its last MFMA (no extra VGPRs), so
-// no pair starts on an LDS round trip; the ring barrier moves to the middle of the pair (ring
-// holds 2 pairs: pair p+2 is staged into pair p's slot once every wave holds A(p) in registers).
-template <int KS, int NPX, bool PF = false>
+template <int KS, int NPX>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -636,7 +477,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int64_t wstep = 4 * wplane;
   const char* const wsrc = (const char*)g.w + (wave / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
   const int wdst = (wave / 2) * PLANE_W + (wave % 2) * 1024;
-  // split-K (tl.ksplit > 1, non-PF only): this workgroup runs input chunks [cb0, cb1)
+  // split-K (tl.ksplit > 1): this workgroup runs input chunks [cb0, cb1)
   const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
   const int split = nsplit > 1 ? (int)blockIdx.y : 0;
   const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
@@ -675,115 +516,10 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
-  if constexpr (PF) {
-    static_assert(NPX % 2 == 0, "block 0 of the next pair lands in bh[0]");
-    constexpr int NPAIR = (KSQ + 1) / 2;
-    constexpr int MID = NPX / 2;
-    const int n_pairs = s.c16 * NPAIR;
-    // pair p = (chunk p / NPAIR, taps 2j, 2j+1) -> ring pair slot p & 1 (2 tap slots); the odd
-    // last tap reloads itself into the second slot (its A is zeroed) to keep 2 copies per pair
-    auto stage_pair = [&](int p) {
-      char* dst = lds + (p & 1) * 2 * SLOT_W + wdst;
-      if (p >= n_pairs) p = n_pairs - 1;
-      const int c = p / NPAIR, j = p - (p / NPAIR) * NPAIR;
-      const int ia = c * KSQ + 2 * j;
-      const int ib = 2 * j + 1 < KSQ ? ia + 1 : ia;
-      glds16((const void*)(wsrc + (int64_t)ia * wstep), dst);
-      glds16((const void*)(wsrc + (int64_t)ib * wstep), dst + SLOT_W);
-    };
-    auto tap_off = [&](int j) -> int {
-      const int tt = 2 * j + 1 < KSQ ? 2 * j + tsel : 2 * j;
-      return (tt / KS) * tl.pitch + (tt - (tt / KS) * KS);
-    };
-    bf16x8g ah[4], al[4], bh[2], bl[2];
-    auto read_a = [&](int p, int cb) {
-      const int j = p - (p / NPAIR) * NPAIR;
-      const char* wsl = lds + (p & 1) * 2 * SLOT_W + tsel * SLOT_W + wlane;
-      ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
-      al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
-      if (2 * j + 1 >= KSQ && tsel) {
-        ah[cb] = bf16x8g{};
-        al[cb] = bf16x8g{};
-      }
-    };
-    stage_pair(1);  // stage_w(0), stage_w(1) above filled tap slots 0, 1 = pair 0
-    int p = 0;
-    for (int c = 0; c < s.c16; ++c) {
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      {
-        const char* src0 = fbase + c * 64 + h_plane * 16;
-        const char* src0_b = fbase_b + c * 64 + h_plane * 16;
-        int hr = h_r0, hc = h_c0;
-        char* dst = halo + h_plane * hplane + h_i0 * 1024;
-        for (int i = h_i0; i < tl.nh; i += 2) {
-          const bool in_a = hr < rowsA;
-          const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
-          const int xx = min(hc - R + s.pin, wp_in - 1);
-          glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
-          dst += 2 * 1024;
-          hc += 2 * 64;
-          while (hc >= tl.pitch) {
-            hc -= tl.pitch;
-            ++hr;
-          }
-        }
-      }
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (c == 0) {
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) read_a(0, cb);
-      }
-      {
-        const int toff = tap_off(0);
-        bh[0] = *(const bf16x8g*)(bplane + (q0(0) + toff) * 16);
-        bl[0] = *(const bf16x8g*)(bplane + hplane + (q0(0) + toff) * 16);
-      }
-#pragma unroll 1
-      for (int j = 0; j < NPAIR; ++j, ++p) {
-        const int toff = tap_off(j);
-#pragma unroll
-        for (int pb = 0; pb < NPX; ++pb) {
-          const int cur = pb & 1;
-          if (pb == MID) {
-            wait_vmcnt<0>();  // pair p+1's copies (staged at the middle of pair p-1) landed ...
-            __builtin_amdgcn_s_barrier();  // ... for every wave; every wave holds A(p): its slot is free
-            asm volatile("" ::: "memory");
-            stage_pair(p + 2);
-          }
-          if (pb + 1 < NPX) {
-            bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
-            bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
-          } else if (j + 1 < NPAIR) {  // block 0 of the next pair (same halo)
-            const int tn = tap_off(j + 1);
-            bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(0) + tn) * 16);
-            bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(0) + tn) * 16);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
-            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-            if (pb == NPX - 1 && p + 1 < n_pairs) {
-              __builtin_amdgcn_sched_barrier(0);
-              read_a(p + 1, cb);  // A(p+1) landed at this pair's barrier; A(p)[cb] is dead
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        }
-      }
-    }
-  } else {
   int it = cb0 * KSQ;
   for (int c = cb0; c < cb1; ++c) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-#ifdef M16_SKIP_RELOAD  // timing experiment only (wrong results): halo loaded for chunk 0 only
-    if (c == 0)
-#endif
     {
       const char* src0 = fbase + c * 64 + h_plane * 16;
       const char* src0_b = fbase_b + c * 64 + h_plane * 16;
@@ -793,7 +529,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(hc - R + s.pin, wp_in - 1);
-        glds16a<M16_HALO_AUX>((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
+        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 2 * 1024;
         hc += 2 * 64;
         while (hc >= tl.pitch) {
@@ -808,19 +544,14 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     bf16x8g ah[4], al[4];
 #pragma unroll 1
     for (int t = 0; t < KSQ; t += 2) {
-#ifndef M16_NO_BARRIER  // timing experiment only (races on the weight ring)
       wait_vmcnt<0>();  // W(it), W(it+1): the newest copies, issued one pair back ...
       __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
       asm volatile("" ::: "memory");
-#endif
       stage_w(it + 2);
       stage_w(it + 3);
       const bool two = t + 1 < KSQ;
       const int tt = two ? t + tsel : t;  // the odd last tap: upper k groups get zero weights
       const char* wsl = lds + ((two ? it + tsel : it) % RING) * SLOT_W + wlane;
-#ifdef M16_ONE_AREAD  // timing experiment only (wrong results): A fragments read once per chunk
-      if (t == 0)
-#endif
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
@@ -837,32 +568,20 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
         const int cur = pb & 1;
-#ifndef M16_ONE_BREAD  // timing experiment only (wrong results): one B fragment per tap pair
         if (pb + 1 < NPX) {
           bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
           bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
         }
-#else
-        bh[cur ^ 1] = bh[cur];
-        bl[cur ^ 1] = bl[cur];
-#endif
         __builtin_amdgcn_sched_barrier(0);
-#ifdef M16_SETPRIO  // timing experiment: MFMA clusters at raised wave priority
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
         }
-#ifdef M16_SETPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
       it += two ? 2 : 1;
     }
-  }
   }
   wait_vmcnt<0>();
 
@@ -1127,7 +846,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
       int hr = lane / tl.pitch, hc = lane - (lane / tl.pitch) * tl.pitch;
       for (int i = 0; i < tl.nh; ++i) {
         const int yy = min(y0 - R + hr + s.pin, hp_in - 1), xx = min(x0 - R + hc + s.pin, wp_in - 1);
-        glds16a<M16K_HALO_AUX>((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
+        glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
         dst += 1024;
         hc += 64;
         while (hc >= tl.pitch) {
@@ -1277,12 +996,12 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 
 // ---- host side ----
 struct BigConfig {
-  int ks, npb, nwave, cw, pair, db = 0, raster = 0, wreg = 0;
+  int ks, npb, nwave, cw, pair, raster = 0;
   int cap_px = 0;  // pixels per tile when npb does not express it (conv_m16 with an odd block count)
   int cap() const { return cap_px ? cap_px : (nwave / (cw / 64)) * npb * 32; }  // pixels per tile
-  int ring_bytes() const { return wreg ? 0 : (pair ? ((raster || ks == 3) ? 4 : 6) : (db ? 2 : 3)) * 4 * cw * 16; }
+  int ring_bytes() const { return (pair ? ((raster || ks == 3) ? 4 : 6) : 3) * 4 * cw * 16; }
   int lds_budget() const { return (nwave == 8 ? 160 : 80) * 1024; }  // 1 or 2 workgroups per CU
-  int halo_budget() const { return (lds_budget() - ring_bytes()) / (db ? 2 : 1); }
+  int halo_budget() const { return lds_budget() - ring_bytes(); }
 };
 
 // LDS halo row pitch (16-B slots): a 32-pixel block that wraps a tile row (tc % 32 != 0) needs
@@ -1290,9 +1009,6 @@ struct BigConfig {
 // every block is one contiguous row segment and the tight tc + ks - 1 suffices.
 static int halo_pitch(int tc, int ks) {
   if (ks == 1) return tc;
-#ifdef BIG_GAP_PITCH  // timing experiment: the gapped pitch everywhere
-  return tc + 16 * ((ks - 1 + 15) / 16);
-#endif
   return tc % 32 == 0 ? tc + ks - 1 : tc + 16 * ((ks - 1 + 15) / 16);
 }
 
@@ -1300,9 +1016,7 @@ static int halo_bytes(int tr, int tc, int ks) {
   return 4 * 1024 * (((tr + ks - 1) * halo_pitch(tc, ks) + 63) / 64);
 }
 
-#ifndef BIG_UTIL_WIN
-#define BIG_UTIL_WIN 0.03
-#endif
+constexpr double BIG_UTIL_WIN = 0.03;
 
 // Pick the tile (tr x tc) that fits LDS: among the tilings within 3 % of the best MFMA-lane
 // utilisation, the one that loads the fewest halo slots per tile pixel (hrows x pitch / (tr tc)).
@@ -1351,20 +1065,19 @@ static bool big_tiling(const BigConfig& k, int n, int h, int w, int groups, int 
   return true;
 }
 
-template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool DB = false, bool RASTER = false,
-          bool WREG = false>
+template <int KS, int NPB, int NWAVE, int CW, int PAIR, bool POOL = false, bool RASTER = false>
 static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const BigTiling& tl, hipStream_t st) {
-  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, DB, RASTER, WREG};
-  const int lds = k.ring_bytes() + (DB ? 2 : 1) * 4 * tl.nh * 1024;
+  const BigConfig k{KS, NPB, NWAVE, CW, PAIR, RASTER};
+  const int lds = k.ring_bytes() + 4 * tl.nh * 1024;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER, WREG>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, RASTER>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, DB, RASTER, WREG>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
+  hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, RASTER>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
@@ -1423,34 +1136,13 @@ static bool raster_tiling(const BigConfig& k, int n, int h, int w, int groups, i
   return true;
 }
 
-// Conv algo 8: the 3x3 c128 layers on double-buffered halos.  Two 4-wave workgroups per CU at
-// 80 KiB each: 2-slot weight ring (16 KiB) + 2 x 32 KiB halos of a 12 x 32 tile.  32-pixel blocks
-// are whole tile rows, so the halo pitch needs no bank-conflict gap: tc + 2 = 34 slots.
-static bool db_tiling(const SplitConvShape& s, int groups, int cop_max, BigTiling& t) {
-  if (s.halo_mode != 8 || s.ks != 3 || cop_max % 128) return false;
-  t.tc = 32;
-  t.tr = 12;
-  t.tiles_x = (s.w + 31) / 32;
-  t.tiles_y = (s.h + t.tr - 1) / t.tr;
-  if ((double)s.w / (t.tiles_x * 32) < 0.9) return false;  // narrow maps (46 wide): single buffer
-  t.pitch = halo_pitch(32, 3);
-  t.hrows = t.tr + 2;
-  t.nh = (t.hrows * t.pitch + 63) / 64;
-  if (2 * 128 * 16 * 4 + 2 * 4 * t.nh * 1024 > 80 * 1024) return false;
-  t.co_tiles = (cop_max + 127) / 128;
-  t.units = groups * t.co_tiles;
-  t.per_unit = s.n * t.tiles_y * t.tiles_x;
-  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
-  return true;
-}
-
-// Default 3x3 c128 layers with c16 even (algos 4, 9-11; 12 keeps conv_big_bf16x3 for them) on
+// Default 3x3 c128 layers with c16 even on
 // conv_m16k_bf16x3 (8 x 32 tiles, 2 workgroups per CU: 32 KiB weight ring + 8-plane halo <= 48
 // KiB; 2-19 % faster per layer than conv_big_bf16x3<3,..> in an interleaved A/B).  false when the
 // shape does not fit (the 46-wide maps, conv1_2's 64 channels).
 static bool m16k_tiling(const SplitConvShape& s, int groups, int cop_max, bool pool, BigTiling& t) {
   const int m = s.halo_mode;
-  if ((m != 4 && m != 9 && m != 10 && m != 11) || s.ks != 3 || cop_max % 128 || (s.c16 & 1) || s.pin < 1)
+  if (m != 4 || s.ks != 3 || cop_max % 128 || (s.c16 & 1) || s.pin < 1)
     return false;
   static const bool no48 = getenv("OP_M16K_NO48") && atoi(getenv("OP_M16K_NO48")) != 0;  // A/B aid
   // 8 x 32 tiles, or 4 x 48 where they waste fewer MFMA lanes (narrow maps; not with the pool)
@@ -1559,13 +1251,7 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
     *taken = 1;
     return launch_m16k(s, g, t, true, st);
   }
-  if (c128 && db_tiling(s, 1, g[0].cop, t)) {
-    *taken = 1;
-    return launch_big_t<3, 6, 4, 128, 0, true, true>(s, g, t, st);
-  }
-  static const int v3 = getenv("OP_BIG3") ? atoi(getenv("OP_BIG3")) : 0;  // tuning aid: 3x3 variant
-  const bool pair = v3 == 3;
-  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, pair} : BigConfig{3, 4, 4, 64, pair};
+  const BigConfig k = c128 ? BigConfig{3, 6, 4, 128, 0} : BigConfig{3, 4, 4, 64, 0};
   t.tc = 32;
   t.tr = k.cap() / 32;  // rows = pixel groups x NPB (even)
   if (halo_bytes(t.tr, t.tc, 3) > k.halo_budget()) return OP_OK;
@@ -1579,7 +1265,6 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
   t.per_unit = s.n * t.tiles_y * t.tiles_x;
   t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
   *taken = 1;
-  if (pair) return c128 ? launch_big_t<3, 6, 4, 128, 1, true>(s, g, t, st) : launch_big_t<3, 4, 4, 64, 1, true>(s, g, t, st);
   if (c128) return launch_big_t<3, 6, 4, 128, 0, true>(s, g, t, st);
   return launch_big_t<3, 4, 4, 64, 0, true>(s, g, t, st);
 }
@@ -1600,8 +1285,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   BigTiling tl{};
   if (s.ks == 7) {
     if (!c128) return OP_OK;
-    if (s.halo_mode != 9 && s.halo_mode != 10 && s.halo_mode != 11 &&
-        raster_tiling(BigConfig{7, 5, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
+    if (raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
       // Tile size per launch shape.  A workgroup's time grows as ~(2 + NPX) (fixed halo /
       // weight-ring / barrier work plus NPX 16-px blocks per wave; measured 0.17 / 0.25 / 0.50 ms
@@ -1631,7 +1315,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
             int best = rounds(tl) * (2 + 10);
             for (int cand : {8, 6, 5, 4, 3, 2}) {
               if (force && cand != force) continue;
-              BigConfig k{7, 1, 8, 128, 1, 0, 1};
+              BigConfig k{7, 1, 8, 128, 1, 1};
               k.cap_px = 64 * cand;
               BigTiling tc{};
               if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
@@ -1649,7 +1333,6 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       static bool attr = false;
-      static const bool pf = getenv("OP_M16_PF") && atoi(getenv("OP_M16_PF")) != 0;
       // Split-K for launches that still leave most CUs idle (one frame, one crop): the input
       // chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce), since a
       // workgroup's time is mostly its per-chunk, per-tap-pair work, not its pixel count
@@ -1657,7 +1340,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       const int wgs = tl.xpu ? 8 * ((tl.per_unit + tl.xpu - 1) / tl.xpu) : tl.units * tl.per_unit;
       tl.ksplit = 1;
       tl.ws = nullptr;
-      if (s.splitk && !(pf && npx == 10)) {
+      if (s.splitk) {
         int S = 1;
         if (ks_force > 0) S = s.c16 % ks_force == 0 ? ks_force : 1;
         else
@@ -1675,8 +1358,8 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         }
       }
       if (!attr) {
-        const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 10, true>,
-                             (const void*)conv_m16_bf16x3<7, 8>,  (const void*)conv_m16_bf16x3<7, 6>,
+        const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 8>,
+                             (const void*)conv_m16_bf16x3<7, 6>,
                              (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
                              (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>};
         for (const void* f : fns)
@@ -1695,11 +1378,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         case 4: hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
         case 3: hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
         case 2: hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        default:
-          if (pf)
-            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          else
-            hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+        default: hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g[0], g1, tl);
       }
       if (tl.ksplit > 1) {
         OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
@@ -1711,19 +1390,10 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       OP_HIP_CHECK(hipGetLastError());
       return OP_OK;
     }
-    if (s.halo_mode == 10) {  // register weights (no ring, no tap barriers), OP_WV_NPB 5 or 6
-      static const int npb = getenv("OP_WV_NPB") ? atoi(getenv("OP_WV_NPB")) : 5;
-      if (raster_tiling(BigConfig{7, npb == 6 ? 6 : 5, 8, 128, 0, 0, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
-        if (plain_order) tl.xpu = 0;
-        *taken = 1;
-        return npb == 6 ? launch_big_t<7, 6, 8, 128, 0, false, false, true, true>(s, g, tl, st)
-                        : launch_big_t<7, 5, 8, 128, 0, false, false, true, true>(s, g, tl, st);
-      }
-    }
-    if (s.halo_mode != 9 && raster_tiling(BigConfig{7, 6, 8, 128, 1, 0, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
+    if (raster_tiling(BigConfig{7, 6, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
       if (plain_order) tl.xpu = 0;
       *taken = 1;
-      return launch_big_t<7, 6, 8, 128, 1, false, false, true>(s, g, tl, st);
+      return launch_big_t<7, 6, 8, 128, 1, false, true>(s, g, tl, st);
     }
     if (!big_tiling(BigConfig{7, 6, 8, 128, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
     if (plain_order) tl.xpu = 0;
@@ -1731,30 +1401,10 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     return launch_big_t<7, 6, 8, 128, 1>(s, g, tl, st);
   }
   if (c128) {
-    static const int v3 = getenv("OP_BIG3") ? atoi(getenv("OP_BIG3")) : 0;  // tuning aid: 3x3 variant
-    if (v3 == 3) {  // 4-wave pairs (2 workgroups per CU, 4-slot ring)
-      const BigConfig k{3, 6, 4, 128, 1};
-      if (!big_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
-      if (plain_order) tl.xpu = 0;
-      *taken = 1;
-      return launch_big_t<3, 6, 4, 128, 1>(s, g, tl, st);
-    }
-    if (v3 == 1 || v3 == 2) {
-      const BigConfig k{3, 6, 8, 128, v3 == 1 ? 1 : 0};
-      if (!big_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
-      if (plain_order) tl.xpu = 0;
-      *taken = 1;
-      return v3 == 1 ? launch_big_t<3, 6, 8, 128, 1>(s, g, tl, st) : launch_big_t<3, 6, 8, 128, 0>(s, g, tl, st);
-    }
     if (m16k_tiling(s, s.groups, cop_max, false, tl)) {
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       return launch_m16k(s, g, tl, false, st);
-    }
-    if (db_tiling(s, s.groups, cop_max, tl)) {
-      if (plain_order) tl.xpu = 0;
-      *taken = 1;
-      return launch_big_t<3, 6, 4, 128, 0, false, true>(s, g, tl, st);
     }
     if (!big_tiling(BigConfig{3, 6, 4, 128, 0}, s.n, s.h, s.w, s.groups, cop_max, tl)) return OP_OK;
     if (plain_order) tl.xpu = 0;

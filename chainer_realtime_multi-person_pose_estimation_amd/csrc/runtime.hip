@@ -623,7 +623,7 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch);
 // one fused launch on the split path with the conv_big families (the pooled tensor is the only
 // output), else the conv into `full` and the pool kernel.
 static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& pooled, const PackedConv& pc, int ch) {
-  if (c->split && (c->conv_algo == 4 || c->conv_algo >= 6)) {
+  if (c->split && c->conv_algo == 4) {
     SplitConvGroup g[2];
     g[0] = sgrp(in, 0, pooled, 0, pc, ch);
     g[1] = g[0];
@@ -634,8 +634,7 @@ static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& poole
     conv_work(c, full, pc, &fl, &by);
     int taken = 0;
     const int rc = profiled(c, conv_class(pc.ks), fl, by, [&] {
-      return c->conv_algo == 7 ? launch_conv_db(sh, g, c->stream, true, &taken)
-                               : launch_conv_big_pool(sh, g, c->stream, &taken);
+      return launch_conv_big_pool(sh, g, c->stream, &taken);
     });
     if (rc || taken) return rc;
   }
@@ -1146,7 +1145,10 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
     return OP_ERR_HIP;
   }
   for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
-  if (const char* e = getenv("OP_HALO_MODE")) op::g_halo_mode = atoi(e);
+  if (const char* e = getenv("OP_HALO_MODE")) {
+    const int m = atoi(e);
+    if (m == 0 || m == 3 || m == 4) op::g_halo_mode = m;
+  }
   c->conv_algo = op::g_halo_mode;
   if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
   if (const char* e = getenv("OP_GUARD")) op::g_guard = ((size_t)atol(e) + 255) / 256 * 256;
@@ -2411,8 +2413,8 @@ int op_set_batch_invariant(op_ctx* c, int32_t enable) {
 int op_set_conv_algo(op_ctx* c, int32_t algo) {
   using namespace op;
   RC(check_ctx(c, false));
-  if (algo < 0 || algo > 12) {
-    set_error("conv algo must be 0..12");
+  if (algo != 0 && algo != 3 && algo != 4) {
+    set_error("conv algo must be 0 (per-tap gather), 3 (co-split halo) or 4 (default)");
     return OP_ERR_INVALID;
   }
   c->conv_algo = algo;

@@ -98,15 +98,12 @@ int op_get_precision(op_ctx* ctx, int32_t* mode);
 /* Kernel family of the bf16x3 convolutions (a tuning knob; every family computes the same
  * products, parity-tested): 4 (default) shared-weight halo tiles (conv_big.hip): the 7x7 layers
  * on v_mfma_f32_16x16x32_bf16 tap pairs over raster tiles (640-pixel ranges of the batch that
- * span frame borders), the 3x3 layers on 16x16x32 with K = 32 input channels over 8 x 32 tiles
- * (32x32x16 kernel for the 46-wide and 64-channel ones); 12 as 4 with every 3x3 layer on the
- * 32x32x16 kernel; 5 the 7x7 as 4, the 3x3 on the gather kernel;
- * 6 the 7x7 on 16x16x32 tap pairs with rectangular tiles (conv_pair.hip), 3x3 as 4;
- * 7 double-buffered 8-channel halos for 7x7 + 3x3 (conv_db.hip); 8 as 4 with the 3x3 c128
- * layers on double-buffered halos; 9 / 11 as 4 with the 7x7 on 32x32x16 rectangular / raster
- * tiles; 10 as 11 with every wave loading its weights into registers (no weight ring);
- * 3 co-split halo tiles (conv_halo.hip); 1 / 2 the 7x7 halo kernel with one / two halo buffers;
- * 0 the per-tap gather kernel.  Shapes a family does not take use the gather kernel. */
+ * span frame borders), the 3x3 layers on 16x16x32 with K = 32 input channels over 8 x 32 / 4 x 48
+ * tiles (32x32x16 kernel for the 64-channel ones), the 1x1 layers on co-split halo tiles;
+ * 3 co-split halo tiles for every layer (conv_halo.hip); 0 the per-tap gather kernel.  Shapes a
+ * family does not take use the gather kernel.  (Round-1 experiment families -- double-buffered
+ * halos, rectangular 7x7 tap pairs, register weights -- live in git history: tools/build_rev.sh
+ * builds that revision as an A/B variant.) */
 int op_set_conv_algo(op_ctx* ctx, int32_t algo);
 /* Batch invariance (default off).  A launch that fills few CUs (one frame, one crop) splits the
  * 7x7 convolutions' input channels over several workgroups and sums their f32 partials, so a

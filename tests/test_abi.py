@@ -5,7 +5,7 @@ import re
 
 import pytest
 
-from conftest import REPO
+from conftest import PKG_NAME, REPO
 
 
 def _declared():
@@ -48,3 +48,13 @@ def test_no_silent_cpu_path(lib):
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         lib.Context(0)
+
+
+def test_library_resolves_its_own_symbols():
+    """Every op:: symbol the library uses is defined in it (a shared library links with undefined
+    symbols; they would only fail at load time on the GPU box)."""
+    import subprocess
+    so = os.path.join(REPO, PKG_NAME, "libopenpose_hip.so")
+    out = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
+    own = [l for l in out.splitlines() if "_ZN2op" in l or " op_" in l]
+    assert not own, own

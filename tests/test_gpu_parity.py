@@ -134,7 +134,7 @@ def test_forward_wide_vs_oracle(ctx, rand_weights, shape):
     _fwd_check(ctx, rand_weights, x)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 3, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("algo", [0, 3])
 def test_conv_algos_agree(ctx, algo):
     """Every bf16x3 kernel family computes the same forward (batch 2 at 368x368 and 720p-shaped
     656x368) as the default family, within the 3xBF16 rounding (the default is held to the oracle
