@@ -23,7 +23,7 @@ EXPORTED = (
     "op_last_error", "op_default_params", "op_default_limits", "op_layer_info", "op_create", "op_destroy",
     "op_set_weights", "op_detect", "op_preprocess", "op_forward", "op_forward_stages", "op_resize_images", "op_compute_peaks",
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
-    "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_synchronize", "op_fetch_result",
+    "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_graph_info", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_host_alloc", "op_host_free",
     "op_pack_results", "op_comm_unique_id", "op_comm_create", "op_comm_destroy", "op_comm_gather_results",
@@ -103,6 +103,7 @@ def lib():
         "op_use_staged_maps": ([P, I32], ctypes.c_int),
         "op_run_staged": ([P], ctypes.c_int),
         "op_run_staged_graph": ([P], ctypes.c_int),
+        "op_graph_info": ([P, P, P, P, P, P], ctypes.c_int),
         "op_run_staged_precise": ([P], ctypes.c_int),
         "op_synchronize": ([P], ctypes.c_int),
         "op_fetch_result": ([P, I32, P, P, I32, P], ctypes.c_int),
@@ -462,6 +463,12 @@ class Context(object):
 
     def synchronize(self):
         check(lib().op_synchronize(self.h), "op_synchronize")
+
+    def graph_info(self):
+        """Node counts of the last captured step graph (op_graph_info)."""
+        v = [ctypes.c_int32() for _ in range(5)]
+        check(lib().op_graph_info(self.h, *[ctypes.byref(x) for x in v]), "op_graph_info")
+        return dict(zip(("nodes", "kernels", "memsets", "memcpys", "host_nodes"), (x.value for x in v)))
 
     def fetch_result(self, frame, cap=2048):
         while True:

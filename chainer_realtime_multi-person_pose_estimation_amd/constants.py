@@ -8,6 +8,8 @@ this path and are not carried.
 """
 from enum import IntEnum
 
+from .nets import CocoPoseNet, FaceNet, HandNet
+
 _JOINT_NAMES = ("Nose Neck RightShoulder RightElbow RightHand LeftShoulder LeftElbow LeftHand "
                 "RightWaist RightKnee RightFoot LeftWaist LeftKnee LeftFoot RightEye LeftEye "
                 "RightEar LeftEar").split()
@@ -19,7 +21,7 @@ _LIMB_PAIRS = ((1, 8), (8, 9), (9, 10), (1, 11), (11, 12), (12, 13), (1, 2), (2,
                (1, 5), (5, 6), (6, 7), (5, 17), (1, 0), (0, 14), (0, 15), (14, 16), (15, 17))
 
 params = dict(
-    archs={"posenet": "CocoPoseNet", "facenet": "FaceNet", "handnet": "HandNet"},
+    archs={"posenet": CocoPoseNet, "facenet": FaceNet, "handnet": HandNet},  # entity.py:50-54: classes
     insize=368,
     downscale=8,
     inference_img_size=368,

@@ -1961,6 +1961,60 @@ int op_run_staged_graph(op_ctx* c) {
   return OP_OK;
 }
 
+static bool host_side(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // unregistered (pageable) host memory
+    return true;
+  }
+  return a.type != hipMemoryTypeDevice;
+}
+
+int op_graph_info(op_ctx* c, int32_t* nodes, int32_t* kernels, int32_t* memsets, int32_t* memcpys,
+                  int32_t* host_nodes) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (!nodes || !kernels || !memsets || !memcpys || !host_nodes) {
+    set_error("op_graph_info: null output");
+    return OP_ERR_INVALID;
+  }
+  if (!c->graph) {
+    set_error("op_graph_info: no captured graph");
+    return OP_ERR_STATE;
+  }
+  size_t n = 0;
+  OP_HIP_CHECK(hipGraphGetNodes(c->graph, nullptr, &n));
+  std::vector<hipGraphNode_t> v(n);
+  OP_HIP_CHECK(hipGraphGetNodes(c->graph, v.data(), &n));
+  *nodes = (int32_t)n;
+  *kernels = *memsets = *memcpys = *host_nodes = 0;
+  for (hipGraphNode_t nd : v) {
+    hipGraphNodeType t;
+    OP_HIP_CHECK(hipGraphNodeGetType(nd, &t));
+    if (t == hipGraphNodeTypeKernel) {
+      ++*kernels;
+    } else if (t == hipGraphNodeTypeMemset) {
+      hipMemsetParams mp;
+      OP_HIP_CHECK(hipGraphMemsetNodeGetParams(nd, &mp));
+      ++*memsets;
+      if (host_side(mp.dst)) ++*host_nodes;
+    } else if (t == hipGraphNodeTypeMemcpy) {
+      hipMemcpy3DParms mp;
+      OP_HIP_CHECK(hipGraphMemcpyNodeGetParams(nd, &mp));
+      ++*memcpys;
+      const void* src = mp.srcArray ? nullptr : mp.srcPtr.ptr;
+      const void* dst = mp.dstArray ? nullptr : mp.dstPtr.ptr;
+      if (mp.kind == hipMemcpyHostToDevice || mp.kind == hipMemcpyDeviceToHost || mp.kind == hipMemcpyHostToHost ||
+          host_side(src) || host_side(dst))
+        ++*host_nodes;
+    } else if (t != hipGraphNodeTypeEmpty) {
+      ++*host_nodes;  // host callbacks, event records / waits, child graphs: not expected
+    }
+  }
+  return OP_OK;
+}
+
 int op_synchronize(op_ctx* c) {
   using namespace op;
   RC(check_ctx(c, false));

@@ -67,22 +67,21 @@ def draw_face_keypoints(orig_img, face_keypoints, left_top):
 
 
 def crop_face(img, rect):
-    """face_detector.py:104-118: rect (x, y, w, h) scaled by face_crop_scale around its centre,
-    clipped to the image, zero-padded to a square; returns (padded_face, (crop_left, crop_top))."""
-    orig_img_h, orig_img_w, _ = img.shape
-    crop_center_x = rect[0] + rect[2] / 2
-    crop_center_y = rect[1] + rect[3] / 2
-    crop_width = rect[2] * params["face_crop_scale"]
-    crop_height = rect[3] * params["face_crop_scale"]
-    crop_left = max(0, int(crop_center_x - crop_width / 2))
-    crop_top = max(0, int(crop_center_y - crop_height / 2))
-    crop_right = min(orig_img_w - 1, int(crop_center_x + crop_width / 2))
-    crop_bottom = min(orig_img_h - 1, int(crop_center_y + crop_height / 2))
-    cropped_face = img[crop_top:crop_bottom, crop_left:crop_right]
-    max_edge_len = np.max(cropped_face.shape[:-1])
-    padded_face = np.zeros((max_edge_len, max_edge_len, cropped_face.shape[-1]), dtype=np.uint8)
-    padded_face[0:cropped_face.shape[0], 0:cropped_face.shape[1]] = cropped_face
-    return padded_face, (crop_left, crop_top)
+    """Restates face_detector.py:104-118: the (x, y, w, h) rect scaled by face_crop_scale about its
+    centre, clipped to [0, W-1) x [0, H-1) like the reference (its right/bottom bound is W-1 / H-1,
+    exclusive), copied into the top-left corner of a zero square whose side is the longer clipped
+    edge.  -> (square crop, (left, top))."""
+    h, w = img.shape[:2]
+    s = params["face_crop_scale"]
+    cx, cy = rect[0] + rect[2] / 2, rect[1] + rect[3] / 2
+    half_w, half_h = rect[2] * s / 2, rect[3] * s / 2
+    x0, x1 = max(0, int(cx - half_w)), min(w - 1, int(cx + half_w))
+    y0, y1 = max(0, int(cy - half_h)), min(h - 1, int(cy + half_h))
+    window = img[y0:y1, x0:x1]
+    side = max(window.shape[:2])
+    square = np.zeros((side, side, window.shape[2]), np.uint8)
+    square[:window.shape[0], :window.shape[1]] = window
+    return square, (x0, y0)
 
 
 def main(argv=None):

@@ -53,3 +53,32 @@ def layers(arch):
     if arch not in LAYERS:
         raise KeyError("unknown arch %r (expected one of %s)" % (arch, sorted(LAYERS)))
     return LAYERS[arch]
+
+
+class _Net(dict):
+    """A network's parameters as {layer: (W, b)}, built like the reference's Chainer models
+    (models/CocoPoseNet.py:23-130, FaceNet.py / HandNet.py:10-76): every conv initialised with
+    Chainer's defaults (LeCunNormal W, zero b; seeded here).  ``params['archs'][arch]()`` returns
+    one, as pose_detector.py:23 expects; the detectors take it as ``model=`` and
+    ``weights.load_npz(path, model)`` fills it in place like ``serializers.load_npz(path, model)``."""
+    arch = None
+
+    def __init__(self, seed=0):
+        from .convert_model import initial_weights
+        super().__init__(initial_weights(self.arch, seed))
+
+    @property
+    def layers(self):
+        return layers(self.arch)
+
+
+class CocoPoseNet(_Net):
+    arch = "posenet"
+
+
+class FaceNet(_Net):
+    arch = "facenet"
+
+
+class HandNet(_Net):
+    arch = "handnet"

@@ -153,40 +153,45 @@ class PoseDetector(object):
             return np.array([]), np.empty(0)
         return poses, scores
 
-    # ---- crops for the face / hand detectors (pose_detector.py:266-425, host-side, used by demo.py) ----
+    # ---- crops for the face / hand detectors (restating pose_detector.py:266-425; host-side, used
+    # by demo.py).  The arithmetic follows the reference operation for operation (the crop SHA-256
+    # fixtures in tests/golden/cpm/ pin it); the structure is this module's own. ----
+
+    # unit-length divisors (pose_detector.py:278-290): nose-neck, shoulder-elbow(R), neck-waist(R),
+    # left ear-shoulder, right ear-shoulder first; every limb's divisor as the fallback
+    _UNIT_BASE = ([14, 3, 0, 13, 9], np.array([0.85, 2.2, 2.2, 0.85, 0.85]))
+    _UNIT_ALL = np.array([2.2, 1.7, 1.7, 2.2, 1.7, 1.7, 0.6, 0.93, 0.65, 0.85, 0.6, 0.93, 0.65, 0.85, 1, 0.2,
+                          0.2, 0.25, 0.25])
+
     def compute_limbs_length(self, joints):
-        """pose_detector.py:266-276 (joint rows are arrays, never None: every limb gets a length)."""
-        limbs = []
-        limbs_len = np.zeros(len(params["limbs_point"]))
-        for i, (a, b) in enumerate(params["limbs_point"]):
-            if joints[a] is not None and joints[b] is not None:
-                limbs.append([joints[a], joints[b]])
-                limbs_len[i] = np.linalg.norm(joints[b][:-1] - joints[a][:-1])
-            else:
-                limbs.append(None)
-        return limbs_len, limbs
+        """pose_detector.py:266-276 -> (lengths (19,) f64, [[joint_a, joint_b] or None per limb]).
+        Rows of a pose array are never None, so every limb gets a length (0 for absent joints at 0,0)."""
+        limbs = [None if joints[a] is None or joints[b] is None else [joints[a], joints[b]]
+                 for a, b in params["limbs_point"]]
+        lengths = np.zeros(len(limbs))
+        for i, limb in enumerate(limbs):
+            if limb is not None:
+                lengths[i] = np.linalg.norm(limb[1][:-1] - limb[0][:-1])
+        return lengths, limbs
 
     def compute_unit_length(self, limbs_len):
-        """pose_detector.py:278-290."""
-        base_limbs_len = limbs_len[[14, 3, 0, 13, 9]]
-        non_zero = base_limbs_len > 0
-        if len(np.nonzero(non_zero)[0]) > 0:
-            ratio = np.array([0.85, 2.2, 2.2, 0.85, 0.85])
-            return np.sum(base_limbs_len[non_zero] / ratio[non_zero]) / len(np.nonzero(non_zero)[0])
-        ratio = np.array([2.2, 1.7, 1.7, 2.2, 1.7, 1.7, 0.6, 0.93, 0.65, 0.85, 0.6, 0.93, 0.65, 0.85, 1, 0.2, 0.2,
-                          0.25, 0.25])
-        non_zero = limbs_len > 0
-        return np.sum(limbs_len[non_zero] / ratio[non_zero]) / len(np.nonzero(non_zero)[0])
+        """pose_detector.py:278-290: mean of length / divisor over the base limbs that were found,
+        else over every limb that was found."""
+        def mean_scaled(lengths, divisors):
+            found = lengths > 0
+            return np.sum(lengths[found] / divisors[found]) / np.count_nonzero(found)
+        idx, div = self._UNIT_BASE
+        base = limbs_len[idx]
+        return mean_scaled(base, div) if np.any(base > 0) else mean_scaled(limbs_len, self._UNIT_ALL)
 
     def get_unit_length(self, person_pose):
         """pose_detector.py:292-296."""
-        limbs_length, _ = self.compute_limbs_length(person_pose)
-        return self.compute_unit_length(limbs_length)
+        return self.compute_unit_length(self.compute_limbs_length(person_pose)[0])
 
     def crop_around_keypoint(self, img, keypoint, crop_size):
-        """pose_detector.py:298-307."""
+        """pose_detector.py:298-307: square of half-size crop_size about keypoint."""
         x, y = keypoint
-        bbox = (int(x - crop_size), int(y - crop_size), int(x + crop_size), int(y + crop_size))
+        bbox = tuple(int(v) for v in (x - crop_size, y - crop_size, x + crop_size, y + crop_size))
         return self.crop_image(img, bbox), bbox
 
     def crop_person(self, img, person_pose, unit_length):
@@ -195,53 +200,38 @@ class PoseDetector(object):
         raise NameError("name 'sys' is not defined")
 
     def crop_face(self, img, person_pose, unit_length):
-        """pose_detector.py:354-369: (face_img, bbox) around the nose, or (None, None)."""
-        face_size = unit_length
-        face_img = None
-        bbox = None
-        if person_pose[JointType.Nose][2] > 0:
-            nose_pos = person_pose[JointType.Nose][:2]
-            face_top = int(nose_pos[1] - face_size * 1.2)
-            face_bottom = int(nose_pos[1] + face_size * 0.8)
-            face_left = int(nose_pos[0] - face_size)
-            face_right = int(nose_pos[0] + face_size)
-            bbox = (face_left, face_top, face_right, face_bottom)
-            face_img = self.crop_image(img, bbox)
-        return face_img, bbox
+        """pose_detector.py:354-369: (face_img, bbox) from 1.2 units above to 0.8 below the nose and
+        one unit either side of it, or (None, None) without a nose."""
+        nx, ny, nv = person_pose[JointType.Nose][:3]
+        if not nv > 0:
+            return None, None
+        bbox = (int(nx - unit_length), int(ny - unit_length * 1.2), int(nx + unit_length), int(ny + unit_length * 0.8))
+        return self.crop_image(img, bbox), bbox
 
     def crop_hands(self, img, person_pose, unit_length):
-        """pose_detector.py:371-399: {'left'|'right': {'img', 'bbox'} or None}.  Like the reference,
-        the crop centre is updated in place in person_pose (``crop_center +=`` on a view)."""
-        hands = {"left": None, "right": None}
+        """pose_detector.py:371-399: {'left'|'right': {'img', 'bbox'} or None}; the centre moves 0.3 of
+        the elbow->hand vector past the hand.  Like the reference, that shift is written into
+        person_pose itself (the centre is a view of the hand row)."""
+        out = {}
         for side, hand, elbow in (("left", JointType.LeftHand, JointType.LeftElbow),
                                   ("right", JointType.RightHand, JointType.RightElbow)):
-            if person_pose[hand][2] > 0:
-                crop_center = person_pose[hand][:-1]
-                if person_pose[elbow][2] > 0:
-                    direction_vec = person_pose[hand][:-1] - person_pose[elbow][:-1]
-                    crop_center += (0.3 * direction_vec).astype(crop_center.dtype)
-                hand_img, bbox = self.crop_around_keypoint(img, crop_center, unit_length * 0.95)
-                hands[side] = {"img": hand_img, "bbox": bbox}
-        return hands
+            out[side] = None
+            if not person_pose[hand][2] > 0:
+                continue
+            centre = person_pose[hand][:-1]  # a view: the in-place shift below reaches person_pose
+            if person_pose[elbow][2] > 0:
+                centre += (0.3 * (person_pose[hand][:-1] - person_pose[elbow][:-1])).astype(centre.dtype)
+            crop, bbox = self.crop_around_keypoint(img, centre, unit_length * 0.95)
+            out[side] = {"img": crop, "bbox": bbox}
+        return {"left": out["left"], "right": out["right"]}
 
     def crop_image(self, img, bbox):
-        """pose_detector.py:401-425: crop clipped to the image, zero-padded to the bbox size."""
+        """pose_detector.py:401-425: the (left, top, right, bottom) box of img; the parts of the box
+        outside the image are zeros."""
         left, top, right, bottom = bbox
-        img_h, img_w, img_ch = img.shape
-        box_h = bottom - top
-        box_w = right - left
-        crop_left = max(0, left)
-        crop_top = max(0, top)
-        crop_right = min(img_w, right)
-        crop_bottom = min(img_h, bottom)
-        crop_h = crop_bottom - crop_top
-        crop_w = crop_right - crop_left
-        cropped_img = img[crop_top:crop_bottom, crop_left:crop_right]
-        bias_x = bias_y = 0
-        if left < crop_left:
-            bias_x = crop_left - left
-        if top < crop_top:
-            bias_y = crop_top - top
-        padded_img = np.zeros((box_h, box_w, img_ch), dtype=np.uint8)
-        padded_img[bias_y:bias_y + crop_h, bias_x:bias_x + crop_w] = cropped_img
-        return padded_img
+        h, w, ch = img.shape
+        out = np.zeros((bottom - top, right - left, ch), np.uint8)
+        y0, y1 = max(0, top), min(h, bottom)
+        x0, x1 = max(0, left), min(w, right)
+        out[y0 - top:y1 - top, x0 - left:x1 - left] = img[y0:y1, x0:x1]
+        return out

@@ -18,6 +18,11 @@ def layer_table(arch="posenet"):
 
 
 def load_npz(path, arch="posenet"):
+    """-> {layer: (W, b)}.  ``load_npz(path, model)`` with a model from nets (``params['archs'][a]()``)
+    fills that model in place and returns it, like ``serializers.load_npz(path, model)``."""
+    model = None
+    if isinstance(arch, nets._Net):
+        model, arch = arch, arch.arch
     with np.load(path, allow_pickle=False) as z:
         keys = list(z.keys())
         out = {}
@@ -29,6 +34,9 @@ def load_npz(path, arch="posenet"):
             W = np.asarray(z[wk[0]], np.float32)
             b = np.asarray(z[bk[0]], np.float32)
             out[name] = (W, b)
+    if model is not None:
+        model.update(out)
+        return model
     return out
 
 

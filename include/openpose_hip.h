@@ -217,6 +217,13 @@ int op_run_staged(op_ctx* ctx);
 int op_run_staged_precise(op_ctx* ctx);
 /* Capture op_run_staged as a hipGraph and replay it (same semantics, fewer launches). */
 int op_run_staged_graph(op_ctx* ctx);
+/* Contents of the step graph op_run_staged_graph captured last (debugging / regression aid; no
+ * reference counterpart): node counts by kind.  host_nodes = memcpy nodes with a host-memory source
+ * or destination, and host / event / other nodes -- none may exist: the step graph touches device
+ * memory only (uploads and result fetches stay outside it, on their own streams / calls).
+ * OP_ERR_STATE when no graph has been captured. */
+int op_graph_info(op_ctx* ctx, int32_t* nodes, int32_t* kernels, int32_t* memsets, int32_t* memcpys,
+                  int32_t* host_nodes);
 int op_synchronize(op_ctx* ctx);
 /* Results of staged frame i (after op_synchronize). */
 int op_fetch_result(op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap, op_frame_result* res);

@@ -158,3 +158,34 @@ def test_cli_writes_npz_loadable_by_pose_detector(tmp_path):
         assert np.array_equal(w[name][0], W) and np.array_equal(w[name][1], b)
     with np.load(str(dst)) as z:
         assert sorted(z.keys()) == sorted(k for n in ref for k in (n + "/W", n + "/b"))
+
+
+def test_copy_lists_match_reference_converter():
+    """nets.CONVERT_LAYERS == models/convert_model.py:8-249's layer_names (extracted from the
+    reference source with ast by tests/golden/make_golden_convert.py), order included."""
+    import json
+    import os
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "convert_layer_names.json")))
+    assert d["source"] == "models/convert_model.py:8-249"
+    assert set(d["layer_names"]) == set(nets.CONVERT_LAYERS) == {"posenet", "facenet", "handnet"}
+    for arch, names in d["layer_names"].items():
+        assert list(nets.CONVERT_LAYERS[arch]) == names, arch
+
+
+def test_params_archs_build_models(tmp_path):
+    """entity.py:50-54 maps arch -> model class and pose_detector.py:23-26 does
+    ``params['archs'][arch]()`` then ``serializers.load_npz(weights_file, model)``."""
+    from conftest import pkg_module as pm
+    params = pm("constants").params
+    for arch, n in (("posenet", 92), ("facenet", 52), ("handnet", 52)):
+        m = params["archs"][arch]()
+        assert len(m) == n and m.arch == arch
+        for name, ci, co, k in nets.layers(arch):
+            W, b = m[name]
+            assert W.shape == (co, ci, k, k) and W.dtype == np.float32 and not b.any()
+    src = weights.random_weights(5)
+    path = str(tmp_path / "w.npz")
+    weights.save_npz(path, src)
+    m = params["archs"]["posenet"]()
+    assert weights.load_npz(path, m) is m
+    assert all(np.array_equal(m[k][0], src[k][0]) and np.array_equal(m[k][1], src[k][1]) for k in src)

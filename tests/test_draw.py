@@ -36,3 +36,18 @@ def test_undetected_joint_breaks_its_limbs():
     pose[0, 8] = (10, 40, 0)  # not detected
     out = D.draw_person_pose(img, pose)
     assert tuple(out[25, 10]) == (0, 0, 0)
+
+
+def test_read_bgr_drops_alpha_like_imread_color():
+    """C1's input, data/person.png (584x584 RGBA, README.md:16): cv2.imread(path) with the default
+    IMREAD_COLOR (pose_detector.py:571) returns the colour channels as BGR and ignores alpha (no
+    compositing); read_bgr must give the same array."""
+    import os
+    from PIL import Image
+    D = pkg_module("draw")
+    path = os.path.join(os.path.dirname(__file__), "golden", "person.png")
+    raw = np.asarray(Image.open(path))
+    assert raw.shape == (584, 584, 4)  # RGBA on disk (opaque alpha)
+    img = D.read_bgr(path)
+    assert img.shape == (584, 584, 3) and img.dtype == np.uint8 and img.flags.c_contiguous
+    assert np.array_equal(img, raw[:, :, 2::-1])
