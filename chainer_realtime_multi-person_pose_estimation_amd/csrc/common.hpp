@@ -121,6 +121,7 @@ struct HaloTiling {
 };
 int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // big-tile 7x7 kernel (conv_big.hip): one workgroup per CU, 128 channels x <= 768 pixels
+int conv_big_device_init(int device);  // per-device constants; call once per context, outside capture
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // 3x3 conv + ReLU + 2x2 max-pool fused (conv_big.hip)
 int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);

@@ -51,6 +51,7 @@ struct BigTiling {
                              // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
   int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
   float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
+  const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
 };
 
 template <int N>
@@ -481,11 +482,17 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
   const int split = nsplit > 1 ? (int)blockIdx.y : 0;
   const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
-  const int n_it = cb1 * KSQ;
+  // ring index it = chunk * KSQP + tap over an even tap count per chunk: the odd 49th tap pairs with
+  // a padding tap whose weights are staged from device zeros, so every pair is a full K = 32 step
+  // (no per-pair masking of the A fragments)
+  constexpr int KSQP = KSQ + (KSQ & 1);
+  const int n_it = cb1 * KSQP;
+  const char* const zsrc = (const char*)tl.zeros + lane * 16;
   auto stage_w = [&](int it) {
     char* dst = lds + (it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
-    glds16((const void*)(wsrc + (int64_t)it * wstep), dst + wdst);
+    const int c = it / KSQP, tp = it - c * KSQP;
+    glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
   };
 
   uint32_t qp[(NPX + 1) / 2];  // this lane's pixel of each block -> halo slot (two per register)
@@ -509,14 +516,14 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  stage_w(cb0 * KSQ);
-  stage_w(cb0 * KSQ + 1);
+  stage_w(cb0 * KSQP);
+  stage_w(cb0 * KSQP + 1);
   const char* const bplane = halo + (2 * khalf) * hplane;             // hi plane; lo at + hplane
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
-  int it = cb0 * KSQ;
+  int it = cb0 * KSQP;
   for (int c = cb0; c < cb1; ++c) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -543,23 +550,19 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     asm volatile("" ::: "memory");
     bf16x8g ah[4], al[4];
 #pragma unroll 1
-    for (int t = 0; t < KSQ; t += 2) {
+    for (int t = 0; t < KSQP; t += 2, it += 2) {
       wait_vmcnt<0>();  // W(it), W(it+1): the newest copies, issued one pair back ...
       __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
       asm volatile("" ::: "memory");
       stage_w(it + 2);
       stage_w(it + 3);
-      const bool two = t + 1 < KSQ;
-      const int tt = two ? t + tsel : t;  // the odd last tap: upper k groups get zero weights
-      const char* wsl = lds + ((two ? it + tsel : it) % RING) * SLOT_W + wlane;
+      // the padding tap (zero weights) reads tap t's pixels: finite values, times zero
+      const int tt = t + tsel < KSQ ? t + tsel : t;
+      const char* wsl = lds + ((it + tsel) % RING) * SLOT_W + wlane;
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
         al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
-        if (!two && tsel) {
-          ah[cb] = bf16x8g{};
-          al[cb] = bf16x8g{};
-        }
       }
       const int toff = (tt / KS) * tl.pitch + (tt - (tt / KS) * KS);
       bf16x8g bh[2], bl[2];
@@ -580,7 +583,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
         }
       }
-      it += two ? 2 : 1;
     }
   }
   wait_vmcnt<0>();
@@ -633,6 +635,30 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       if (o32) *(floatx4*)(o32 + co) = v;
     }
   }
+}
+
+// Device zeros per HIP device (the 7x7 padding tap's weights), allocated outside any stream capture
+// by conv_big_device_init() when a context is created.
+static std::mutex g_zeros_mu;
+static std::map<int, void*> g_zeros;
+
+int conv_big_device_init(int device) {
+  std::lock_guard<std::mutex> lk(g_zeros_mu);
+  if (g_zeros.count(device)) return OP_OK;
+  void* z = nullptr;
+  OP_HIP_CHECK(hipMalloc(&z, 4096));
+  OP_HIP_CHECK(hipMemset(z, 0, 4096));
+  OP_HIP_CHECK(hipDeviceSynchronize());
+  g_zeros[device] = z;
+  return OP_OK;
+}
+
+static const void* device_zeros() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_zeros_mu);
+  auto it = g_zeros.find(d);
+  return it == g_zeros.end() ? nullptr : it->second;
 }
 
 // Per-stream split-K workspace, owned by the context that owns the stream: grown on demand
@@ -1331,6 +1357,11 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         }
       }
       if (plain_order) tl.xpu = 0;
+      tl.zeros = device_zeros();
+      if (!tl.zeros) {
+        set_error("conv_m16_bf16x3: conv_big_device_init was not called for this device");
+        return OP_ERR_STATE;
+      }
       *taken = 1;
       static bool attr = false;
       // Split-K for launches that still leave most CUs idle (one frame, one crop): the input

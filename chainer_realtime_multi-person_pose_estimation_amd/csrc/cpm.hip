@@ -449,6 +449,11 @@ int op_cpm_create(int32_t arch, int32_t device, op_cpm_ctx** out) {
     set_error("op_cpm_create: stream");
     return OP_ERR_HIP;
   }
+  if (conv_big_device_init(device) != OP_OK) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return OP_ERR_HIP;
+  }
   std::vector<double> w;
   c->gauss_r = gaussian_taps(2.5, w);  // params['gaussian_sigma'] (entity.py:77)
   OP_HIP_CHECK(hipMalloc(&c->d_gauss, w.size() * sizeof(double)));

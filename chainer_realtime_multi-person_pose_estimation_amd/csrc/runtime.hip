@@ -1144,6 +1144,11 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
     delete c;
     return OP_ERR_HIP;
   }
+  if (op::conv_big_device_init(device) != OP_OK) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return OP_ERR_HIP;
+  }
   for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
   if (const char* e = getenv("OP_HALO_MODE")) {
     const int m = atoi(e);
