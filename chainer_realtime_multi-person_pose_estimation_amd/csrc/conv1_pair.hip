@@ -117,7 +117,14 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
       const int grp = __builtin_amdgcn_readfirstlane(it / kP1Items);
       const int s = it - grp * kP1Items;
       if (s >= kP1Slots) continue;
-      const int ry = s / kP1HC, rx = s - (s / kP1HC) * kP1HC;
+      // slot order: the 32 leading columns row by row (a 32-lane group reads one row of the input
+      // window: consecutive words, no bank conflict), then the last 2 columns of every row (in
+      // plain row-major order most groups straddle a row end, where the window pitch 36 skips 2
+      // words: 2-way conflicts on every conv1_1 input read)
+      constexpr int kLead = kP1HR * 32;  // 320 slots of the leading 32 columns
+      const int ry = s < kLead ? s >> 5 : (s - kLead) >> 1;
+      const int rx = s < kLead ? s & 31 : 32 + ((s - kLead) & 1);
+      const int hs = ry * kP1HC + rx;  // halo slot
       const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
       const int cbase = 32 * half + 16 * grp;
       u16x8p hv[2], lv[2];
@@ -154,8 +161,8 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
       // planes: chunk grp, k-half k, hi / lo
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        *(u16x8p*)(halo + (grp * 4 + 2 * k) * kP1Plane + s * 16) = hv[k];
-        *(u16x8p*)(halo + (grp * 4 + 2 * k + 1) * kP1Plane + s * 16) = lv[k];
+        *(u16x8p*)(halo + (grp * 4 + 2 * k) * kP1Plane + hs * 16) = hv[k];
+        *(u16x8p*)(halo + (grp * 4 + 2 * k + 1) * kP1Plane + hs * 16) = lv[k];
       }
     }
     __syncthreads();
