@@ -255,6 +255,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("OP_BENCH_DEVICE"):  # rehearsal aid: every rank on one device (RCCL then refuses
+        local = int(os.environ["OP_BENCH_DEVICE"])  # the duplicate GPU and the labelled TCP gather runs)
     import importlib
     L = importlib.import_module(PKG + "._lib")
     Wm = importlib.import_module(PKG + ".weights")
