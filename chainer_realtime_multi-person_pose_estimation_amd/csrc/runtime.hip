@@ -150,6 +150,7 @@ struct ProfPair {
   int cls;
   hipEvent_t a, b;
   double flops, bytes;
+  int n;  // launches between a and b (a joined run of back-to-back launches of one class)
 };
 
 // Logical input channel of physical channel p in the stage-input buffer (-1 = zero pad).
@@ -299,6 +300,10 @@ struct op_ctx {
   bool prof = false;
   int splitk = 1;  // op_set_batch_invariant(0): small 7x7 launches may split K
   int prof_mask = 0xF;  // kernel classes timed while prof (op_profile_classes)
+  // set by the forward around launches it issues back to back (the 7x7 Mconv1..Mconv5 of a stage):
+  // a profiled launch then extends the previous pair of its class instead of adding an event pair
+  // (an event record between two kernels costs ~10 us of stream idle time on this runtime)
+  bool prof_join = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<op::ProfPair> pending;
@@ -540,12 +545,21 @@ static hipEvent_t pool_event(op_ctx* c) {
 template <class Fn>
 static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
   if (!c->prof || !((c->prof_mask >> cls) & 1)) return fn();
+  if (c->prof_join && !c->pending.empty() && c->pending.back().cls == cls) {
+    ProfPair& p = c->pending.back();  // the previous launch of this run ended with p.b: move p.b past fn
+    const int rc = fn();
+    OP_HIP_CHECK(hipEventRecord(p.b, c->stream));
+    p.flops += flops;
+    p.bytes += bytes;
+    p.n += 1;
+    return rc;
+  }
   hipEvent_t a = pool_event(c), b = pool_event(c);
   if (!a || !b) return fn();
   OP_HIP_CHECK(hipEventRecord(a, c->stream));
   const int rc = fn();
   OP_HIP_CHECK(hipEventRecord(b, c->stream));
-  c->pending.push_back(ProfPair{cls, a, b, flops, bytes});
+  c->pending.push_back(ProfPair{cls, a, b, flops, bytes, 1});
   return rc;
 }
 
@@ -801,10 +815,16 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
     RC(conv1(c, cat, 0, B[B_BRA], 0, c->st_first[st], 256, true));
     const Act* src = &B[B_BRA];
     const Act* dst = &B[B_BRB];
+    c->prof_join = true;  // Mconv2..Mconv5 follow Mconv1 back to back on the stream
     for (int i = 0; i < 4; ++i) {
-      RC(conv2(c, *src, 0, 128, *dst, 0, 128, c->st_g[st][0][i], c->st_g[st][1][i], 128, 128, true));
+      const int r = conv2(c, *src, 0, 128, *dst, 0, 128, c->st_g[st][0][i], c->st_g[st][1][i], 128, 128, true);
+      if (r) {
+        c->prof_join = false;
+        return r;
+      }
       std::swap(src, dst);
     }
+    c->prof_join = false;
     // the last stage also leaves a dense f32 copy (paf at 0, heat at 40) for the post-process
     const Act* m32 = (c->split && (st == 4 || stages)) ? &B[B_MAP32] : nullptr;
     const PackedConv a[2] = {c->st_g[st][0][4], c->st_g[st][1][4]}, b[2] = {c->st_last[st][0], c->st_last[st][1]};
@@ -2531,7 +2551,7 @@ int op_profile_read(op_ctx* c, int32_t cls, double* ms, int64_t* launches, doubl
     float t = 0.0f;
     OP_HIP_CHECK(hipEventElapsedTime(&t, p.a, p.b));
     c->prof_ms[p.cls] += t;
-    c->prof_n[p.cls] += 1;
+    c->prof_n[p.cls] += p.n;
     c->prof_flops[p.cls] += p.flops;
     c->prof_bytes[p.cls] += p.bytes;
   }
