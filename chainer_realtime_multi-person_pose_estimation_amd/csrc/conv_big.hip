@@ -410,6 +410,50 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   }
 }
 
+// Epilogue of the 16x16x32 kernels: a lane holds 4 consecutive output channels c..c+3 of one pixel
+// (D rows = channels, row kg = lane / 16), so rows kg and kg ^ 1 together hold one 8-channel group
+// whose split record is [hi c..c+7 (16 B)][lo c..c+7 (16 B)].  own = this lane's {hi, hi, lo, lo}
+// dwords; w = the same after v_permlane16_swap (odd rows of the hi operand <-> even rows of the lo
+// operand): the even row then holds the group's 16 hi bytes and the odd row its 16 lo bytes, so one
+// 16-B store per lane replaces two 8-B stores.  Every lane of the wave must execute this.
+__device__ __forceinline__ void split_pair_swap(const floatx4& acc, const floatx4& bv, int relu, floatx4& v,
+                                                uint32_t own[4], uint32_t w[4]) {
+  unsigned short hb[4], lb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float fv = acc[e] + bv[e];
+    if (relu) fv = fv > 0.0f ? fv : 0.0f;
+    v[e] = fv;
+    const __bf16 h16 = (__bf16)fv;
+    const __bf16 l16v = (__bf16)(fv - (float)h16);
+    hb[e] = __builtin_bit_cast(unsigned short, h16);
+    lb[e] = __builtin_bit_cast(unsigned short, l16v);
+  }
+  own[0] = hb[0] | ((uint32_t)hb[1] << 16);
+  own[1] = hb[2] | ((uint32_t)hb[3] << 16);
+  own[2] = lb[0] | ((uint32_t)lb[1] << 16);
+  own[3] = lb[2] | ((uint32_t)lb[3] << 16);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(own[0], own[2], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(own[1], own[3], false, false);
+  w[0] = r0[0];
+  w[1] = r1[0];
+  w[2] = r0[1];
+  w[3] = r1[1];
+}
+
+// Store one lane's part of an 8-channel group (see split_pair_swap): one 16-B store when the whole
+// group is stored, else (a group cut by cout_store) this lane's own two 8-B pieces.
+__device__ __forceinline__ void store_split_group(char* optr, int co, int kg, int cout_store, const uint32_t own[4],
+                                                  const uint32_t w[4]) {
+  char* gp = optr + (co >> 3) * 32;
+  if ((co | 7) < cout_store) {
+    *(uint4*)(gp + (kg & 1) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    *(uint2*)(gp + (co & 7) * 2) = make_uint2(own[0], own[1]);
+    *(uint2*)(gp + 16 + (co & 7) * 2) = make_uint2(own[2], own[3]);
+  }
+}
+
 // ---- 7x7 on v_mfma_f32_16x16x32_bf16, raster tiles (the default 7x7 kernel) ----
 // K = 32 of the 16x16x32 form is fed with a tap PAIR of one 16-channel chunk: lane group
 // g = lane / 16 holds k = 8g..8g+7 = tap t + g/2, channel half g%2, so halo and weight ring keep
@@ -607,7 +651,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
     const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    if (P > P1) continue;
     const int f = P / tl.hw, pp = P - f * tl.hw;
     const int y = pp / s.w, x = pp - y * s.w;
     char* optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
@@ -615,23 +658,12 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-      if (co >= g.cout_store) continue;
-      const floatx4 bv = *(const floatx4*)(g.bias + co);
       floatx4 v;
-      u16x4g vh, vl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float fv = acc[cb][pb][e] + bv[e];
-        if (s.relu) fv = fv > 0.0f ? fv : 0.0f;
-        v[e] = fv;
-        const __bf16 h16 = (__bf16)fv;
-        const __bf16 l16v = (__bf16)(fv - (float)h16);
-        vh[e] = __builtin_bit_cast(unsigned short, h16);
-        vl[e] = __builtin_bit_cast(unsigned short, l16v);
-      }
-      char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
-      *(u16x4g*)d = vh;
-      *(u16x4g*)(d + 16) = vl;
+      uint32_t own[4], w[4];
+      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
+                      v, own, w);
+      if (P > P1 || co >= g.cout_store) continue;
+      store_split_group(optr, co, kg, g.cout_store, own, w);
       if (o32) *(floatx4*)(o32 + co) = v;
     }
   }
@@ -991,30 +1023,19 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
   for (int pb = 0; pb < NPX; ++pb) {
     const int b = pg * NPX + pb;
     const int r = b / TCB, c = (b % TCB) * 16 + l16;
-    if (r >= rows_here || c >= cols_here) continue;
+    const bool live = r < rows_here && c < cols_here;
     const int y = y0 + r, x = x0 + c;
     char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
     float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-      if (co >= g.cout_store) continue;
-      const floatx4 bv = *(const floatx4*)(g.bias + co);
       floatx4 v;
-      u16x4g vh, vl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float fv = acc[cb][pb][e] + bv[e];
-        if (s.relu) fv = fv > 0.0f ? fv : 0.0f;
-        v[e] = fv;
-        const __bf16 h16 = (__bf16)fv;
-        const __bf16 l16v = (__bf16)(fv - (float)h16);
-        vh[e] = __builtin_bit_cast(unsigned short, h16);
-        vl[e] = __builtin_bit_cast(unsigned short, l16v);
-      }
-      char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
-      *(u16x4g*)d = vh;
-      *(u16x4g*)(d + 16) = vl;
+      uint32_t own[4], w[4];
+      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
+                      v, own, w);
+      if (!live || co >= g.cout_store) continue;
+      store_split_group(optr, co, kg, g.cout_store, own, w);
       if (o32) *(floatx4*)(o32 + co) = v;
     }
   }
