@@ -473,7 +473,10 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   constexpr int SLOT_W = 4 * PLANE_W;
   constexpr int RING = 4;
   constexpr int CAP = PG * NPX * 16;
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [W ring][halo: 4 planes]
+  // halo planes at a fixed 32-KiB stride (raster_tiling keeps nh <= 32), placed first so a lane's
+  // lo-plane read is its hi-plane address + an immediate offset; the weight ring follows
+  constexpr int HPLANE = 32 * 1024;
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
 
   const int lin = blockIdx.x;
   int unit, widx;
@@ -509,8 +512,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int ch = wave / PG, pg = wave % PG;
   const int l16 = lane & 15, kg = lane >> 4;  // k group: tap t + kg/2, channel half kg%2
   const int tsel = kg >> 1, khalf = kg & 1;
-  const int hplane = tl.nh * 1024;
-  char* const halo = lds + RING * SLOT_W;
+  char* const halo = lds;
+  char* const ring = lds + 4 * HPLANE;
   const int wp_in = s.w + 2 * s.pin;
   const int hp_in = s.h + 2 * s.pin;
   const int64_t pix_bytes = (int64_t)s.cs_in * 4;
@@ -533,26 +536,26 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int n_it = cb1 * KSQP;
   const char* const zsrc = (const char*)tl.zeros + lane * 16;
   auto stage_w = [&](int it) {
-    char* dst = lds + (it % RING) * SLOT_W;
+    char* dst = ring + (it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
     const int c = it / KSQP, tp = it - c * KSQP;
     glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
   };
 
-  uint32_t qp[(NPX + 1) / 2];  // this lane's pixel of each block -> halo slot (two per register)
+  // this lane's pixel of each block -> byte offset of its halo slot in its hi plane (2 khalf), so
+  // a B fragment address is qb[pb] + the tap's offset: one VALU add per block
+  int qb[NPX];
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
     const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    uint32_t q = 0u;
+    int q = 0;
     if (P <= P1) {
       const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
       const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
-      q = (uint32_t)((f == frame ? y - y0 : rowsA + y) * tl.pitch + x);
+      q = (f == frame ? y - y0 : rowsA + y) * tl.pitch + x;
     }
-    if (pb & 1) qp[pb >> 1] |= q << 16;
-    else qp[pb >> 1] = q;
+    qb[pb] = (2 * khalf) * HPLANE + q * 16;
   }
-  auto q0 = [&](int pb) -> int { return (int)((qp[pb >> 1] >> (16 * (pb & 1))) & 0xffffu); };
 
   floatx4 acc[4][NPX];
 #pragma unroll
@@ -562,7 +565,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 
   stage_w(cb0 * KSQP);
   stage_w(cb0 * KSQP + 1);
-  const char* const bplane = halo + (2 * khalf) * hplane;             // hi plane; lo at + hplane
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       const char* src0 = fbase + c * 64 + h_plane * 16;
       const char* src0_b = fbase_b + c * 64 + h_plane * 16;
       int hr = h_r0, hc = h_c0;
-      char* dst = halo + h_plane * hplane + h_i0 * 1024;
+      char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
       for (int i = h_i0; i < tl.nh; i += 2) {
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
@@ -600,24 +602,28 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       asm volatile("" ::: "memory");
       stage_w(it + 2);
       stage_w(it + 3);
-      // the padding tap (zero weights) reads tap t's pixels: finite values, times zero
-      const int tt = t + tsel < KSQ ? t + tsel : t;
-      const char* wsl = lds + ((it + tsel) % RING) * SLOT_W + wlane;
+      // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
+      // tap (zero weights) reads tap t's pixels: finite values, times zero
+      const int t1 = t + 1 < KSQ ? t + 1 : t;
+      const int toff0 = ((t / KS) * tl.pitch + (t - (t / KS) * KS)) * 16;
+      const int toff1 = ((t1 / KS) * tl.pitch + (t1 - (t1 / KS) * KS)) * 16;
+      const int toff = tsel ? toff1 : toff0;
+      const char* wsl = ring + (((unsigned)(it + tsel) & (RING - 1)) * SLOT_W) + wlane;
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
         al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
       }
-      const int toff = (tt / KS) * tl.pitch + (tt - (tt / KS) * KS);
       bf16x8g bh[2], bl[2];
-      bh[0] = *(const bf16x8g*)(bplane + (q0(0) + toff) * 16);
-      bl[0] = *(const bf16x8g*)(bplane + hplane + (q0(0) + toff) * 16);
+      bh[0] = *(const bf16x8g*)(halo + qb[0] + toff);
+      bl[0] = *(const bf16x8g*)(halo + qb[0] + toff + HPLANE);
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
         const int cur = pb & 1;
         if (pb + 1 < NPX) {
-          bh[cur ^ 1] = *(const bf16x8g*)(bplane + (q0(pb + 1) + toff) * 16);
-          bl[cur ^ 1] = *(const bf16x8g*)(bplane + hplane + (q0(pb + 1) + toff) * 16);
+          const char* bp = halo + qb[pb + 1] + toff;
+          bh[cur ^ 1] = *(const bf16x8g*)bp;
+          bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1418,7 +1424,11 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
           OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
       }
-      const int lds = 4 * 4 * 128 * 16 + 4 * tl.nh * 1024;
+      if (tl.nh > 32) {
+        set_error("conv_m16_bf16x3: halo plane over 32 KiB");
+        return OP_ERR_INVALID;
+      }
+      const int lds = 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes at a fixed 32-KiB stride
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
