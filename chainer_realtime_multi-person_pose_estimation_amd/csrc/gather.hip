@@ -221,6 +221,15 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
   OP_HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_packed[k], 0));
   ncclResult_t r = ncclGather(g->d_rec[k], g->rank == 0 ? g->d_all[k] : nullptr, mine, ncclUint8, 0, g->comm, g->stream);
   if (r != ncclSuccess && r != ncclInProgress) return nccl_fail("ncclGather", r);
+  if (r == ncclInProgress) {
+    // non-blocking communicator: the gather may still be on its way into g->stream; the root's D2H
+    // copy must be enqueued behind it, so wait until RCCL reports the call complete (bounded)
+    RC(wait_for(g, 300.0, "ncclGather enqueue", [&]() -> int {
+      ncclResult_t ae = ncclInProgress;
+      if (ncclCommGetAsyncError(g->comm, &ae) != ncclSuccess) return -1;
+      return ae == ncclSuccess ? 1 : 0;  // an error state is reported (and aborted) by wait_for
+    }));
+  }
   if (g->rank == 0) OP_HIP_CHECK(hipMemcpyAsync(g->h_all[k], g->d_all[k], all, hipMemcpyDeviceToHost, g->stream));
   OP_HIP_CHECK(hipEventRecord(g->ev_done[k], g->stream));
   g->queued[k] = n * g->world;
