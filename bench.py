@@ -226,9 +226,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=38,
-                    help="frames per step per GPU (38: the 7x7 kernel's 640-pixel raster tiles, "
-                         "ceil(38 x 2116 / 640) = 126 per branch x 2 = 252 workgroups, one per CU)")
+    ap.add_argument("--batch", type=int, default=114,
+                    help="frames per step per GPU (114 = 3 x 38: the 7x7 kernel's 640-pixel raster tiles, "
+                         "ceil(38 x 2116 / 640) = 126 per branch x 2 = 252 workgroups = one per CU, in three "
+                         "rounds per launch; measured 1678 / 1709 / 1727 / 1730 frames/s at 38 / 76 / 114 / "
+                         "152-228, profiles/r02/batch_sweep_r02.log)")
     ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
                     help="post-process input: COCO-like multi-person maps (default) or the random-weight "
                          "network's own last stage")
