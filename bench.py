@@ -226,8 +226,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=114,
-                    help="frames per step per GPU (114 = 3 x 38: the 7x7 kernel's 640-pixel raster tiles, "
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step per GPU; default 114 for the 368x368 headline, 63 for 1280x720 single "
+                         "scale, 16 for --precise.  114 = 3 x 38: the 7x7 kernel's 640-pixel raster tiles, "
                          "ceil(38 x 2116 / 640) = 126 per branch x 2 = 252 workgroups = one per CU, in three "
                          "rounds per launch; measured 1678 / 1709 / 1727 / 1730 frames/s at 38 / 76 / 114 / "
                          "152-228, profiles/r02/batch_sweep_r02.log)")
@@ -266,6 +267,8 @@ def main():
     transport = Fr.SocketTransport(rank, world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
                                    timeout=300.0) if world > 1 else None
 
+    if args.batch is None:  # three rounds of full-chip 7x7 launches per step (single scale); C4: 16 frames
+        args.batch = 16 if args.precise else (114 if (FH, FW) == (368, 368) else 63)
     B = args.batch
     net_w, net_h = optimal_size(FH, FW)
     halo_mode = int(os.environ.get("OP_HALO_MODE", "4"))
