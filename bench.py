@@ -136,17 +136,28 @@ def committed_traffic(kernel, batch, precision, halo_mode):
 
 class Runner(object):
     """One configuration's step loop on this rank: async uploads from a 2-batch pinned pool, the
-    staged path (single scale or precise), result fetch, N > 1 gather of the previous step."""
+    staged path (single scale or precise), and the step's results to the host.
 
-    def __init__(self, L, ctx, args, B, FH, FW, rank, world, gather):
-        self.L, self.ctx, self.args, self.B, self.rank, self.world, self.gather = L, ctx, args, B, rank, world, gather
+    Device path (default, any N): after the post-process the step's per-frame result records are
+    packed in HBM and gathered to rank 0 on a communicator stream (an RCCL communicator of one rank
+    at N = 1), landing in pinned memory; the host collects step k-1's records while the GPU runs
+    step k, so no per-step host synchronisation idles the GPU.  Host path (the labelled fallback
+    when RCCL refuses the setup): synchronous op_fetch_results + the TCP gather."""
+
+    def __init__(self, L, Fr, ctx, args, B, FH, FW, rank, world, gather):
+        self.L, self.Fr, self.ctx, self.args, self.B = L, Fr, ctx, args, B
+        self.rank, self.world, self.gather = rank, world, gather
         rng = np.random.default_rng(1234 + rank)
         self.pool = [L.PinnedFrames(B, FH, FW) for _ in range(2)]
         for p in self.pool:
             p.array[...] = rng.integers(0, 256, (B, FH, FW, 3), dtype=np.uint8)
         self.k = 0
         self.persons = 0
-        self.outstanding = 0
+        self.over_caps = 0  # device-path frames whose record says "over the batched caps" (never re-run)
+        # host path: the TCP fallback, detect_precise (full-resolution results), and workloads that
+        # may exceed the batched post-process caps (fetch_results re-runs those frames uncapped)
+        self.sync = not gather.device or bool(args.precise)
+        self.pending = []  # collect flags of the gathers in flight (oldest first)
         self.ctx.upload_frames(self.pool[0].array)
 
     def step(self, collect):
@@ -155,27 +166,42 @@ class Runner(object):
             ctx.run_staged_precise()
         else:
             ctx.run_staged(graph=bool(a.graph))
-        if self.world > 1 and self.gather.device:
-            self.gather.g.submit(0, B, self.k * B * self.world + self.rank, self.world)
-        ctx.upload_frames(self.pool[(self.k + 1) % 2].array)  # next step's frames, overlapped
-        ctx.synchronize()
-        res = ctx.fetch_results(0, B)
-        if collect:
-            self.persons += sum(r[2].n_persons for r in res)
-        if self.world > 1:
-            if not self.gather.device:
-                self.gather.g.submit([(self.k * B * self.world + self.rank + i * self.world, r[2].status,
-                                       r[2].n_peaks, r[0], r[1]) for i, r in enumerate(res)])
-            self.outstanding += 1
-            if self.outstanding == 2:  # collect step k-1's gather (step k's is in flight)
-                self.gather.g.wait()
-                self.outstanding -= 1
+        base = self.k * B * self.world + self.rank
+        if not self.sync:
+            self.gather.g.submit(0, B, base, self.world)
+            ctx.upload_frames(self.pool[(self.k + 1) % 2].array)  # next step's frames, overlapped
+            self.pending.append(collect)
+            if len(self.pending) == 2:  # collect step k-1's records (step k is in flight)
+                self._collect()
+        else:
+            ctx.upload_frames(self.pool[(self.k + 1) % 2].array)
+            ctx.synchronize()
+            res = ctx.fetch_results(0, B)
+            if collect:
+                self.persons += sum(r[2].n_persons for r in res)
+            if self.world > 1 and not self.gather.device:
+                self.gather.g.submit([(base + i * self.world, r[2].status, r[2].n_peaks, r[0], r[1])
+                                      for i, r in enumerate(res)])
+                self.pending.append(False)
+                if len(self.pending) == 2:
+                    self.gather.g.wait()
+                    self.pending.pop(0)
         self.k += 1
 
+    def _collect(self):
+        raw = self.gather.g.wait(raw=True)
+        if self.pending.pop(0) and raw is not None:  # rank 0: every rank's records of that step
+            persons, over = self.Fr.count_persons(raw, GATHER_PERSONS)
+            self.persons += persons
+            self.over_caps += over
+
     def drain(self):
-        while self.outstanding:
-            self.gather.g.wait()
-            self.outstanding -= 1
+        while self.pending:
+            if not self.sync:
+                self._collect()
+            else:
+                self.gather.g.wait()
+                self.pending.pop(0)
 
     def close(self):
         for p in self.pool:
@@ -188,12 +214,16 @@ class Gather(object):
 
 
 def make_gather(Fr, ctx, transport, world):
-    if world == 1:
-        return Gather(None, False, "single GPU (no gather)")
     try:
-        return Gather(Fr.RcclGather(ctx, transport, GATHER_PERSONS, timeout=300.0), True,
-                      "frame-parallel x%d, RCCL ncclGather of per-frame result records from HBM to rank 0" % world)
-    except Exception as e:  # labelled, never silent: the scaling line says which transport ran
+        g = Fr.RcclGather(ctx, transport, GATHER_PERSONS, timeout=300.0)
+        if world == 1:
+            return Gather(g, True, "single GPU (results packed in HBM, copied to pinned memory on a side "
+                                   "stream, collected one step behind)")
+        return Gather(g, True, "frame-parallel x%d, RCCL ncclGather of per-frame result records from HBM to "
+                               "rank 0" % world)
+    except Exception as e:  # labelled, never silent: the line says which transport ran
+        if world == 1:
+            return Gather(None, False, "single GPU (synchronous result fetch: RCCL unavailable: %s)" % e)
         return Gather(Fr.HostGather(transport, GATHER_PERSONS), False,
                       "frame-parallel x%d, TCP gather of result records (RCCL init failed: %s)" % (world, e))
 
@@ -265,7 +295,7 @@ def main():
     Wm = importlib.import_module(PKG + ".weights")
     Fr = importlib.import_module(PKG + ".frames")
     transport = Fr.SocketTransport(rank, world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                                   timeout=300.0) if world > 1 else None
+                                   timeout=300.0)  # world 1: no sockets; bootstrap of the 1-rank gather
 
     if args.batch is None:  # three rounds of full-chip 7x7 launches per step (single scale); C4: 16 frames
         args.batch = 16 if args.precise else (114 if (FH, FW) == (368, 368) else 63)
@@ -288,7 +318,7 @@ def main():
         ctx.stage_maps(np.ascontiguousarray(np.repeat(m[None], B, axis=0)))
         ctx.use_staged_maps(True)
     gather = make_gather(Fr, ctx, transport, world)
-    run = Runner(L, ctx, args, B, FH, FW, rank, world, gather)
+    run = Runner(L, Fr, ctx, args, B, FH, FW, rank, world, gather)
     elapsed, prof = measure(run, ctx, transport, args.steps, args.warmup,
                             not args.no_profile and not args.graph)
     persons = run.persons
@@ -303,9 +333,11 @@ def main():
     ctx.synchronize()
     prof_all = ctx.profile_read()
     ctx.profile(False)
+    over_caps = run.over_caps
     if transport:
         elapsed = transport.all_reduce(elapsed, "max")
         persons = transport.all_reduce(float(persons), "sum")
+        over_caps = transport.all_reduce(float(over_caps), "sum")
 
     frames_total = world * B * args.steps
     value = frames_total / elapsed
@@ -350,6 +382,7 @@ def main():
                    "heatmap": "%dx%d" % optimal_size(FH, FW, 320) if not args.precise else "%dx%d" % (FW, FH),
                    "maps": args.maps, "parallelism": gather.label},
         "persons_per_s": round(persons / elapsed, 2),
+        "frames_over_caps": int(over_caps),  # device-record path: frames past the batched post-process caps
         "gflop_per_frame": round((sum(L.forward_flops(*precise_net(FH, FW, sc)) for sc in PARAMS_SCALES)
                                   if args.precise else L.forward_flops(net_h, net_w)) / 1e9, 2),
         "stage_ms_per_step": stage_ms,
@@ -361,7 +394,9 @@ def main():
         variants = {}
         vsteps = 5
         ctx.use_staged_maps(False)
+        run.sync = True  # the random network's maps can exceed the batched caps: fetch_results re-runs those
         e, _ = measure(run, ctx, None, vsteps, 1, False)
+        run.sync = not gather.device or bool(args.precise)
         variants["maps_network"] = {"value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
                                     "note": "post-process on the random network's own last-stage maps"}
         if args.maps == "synthetic":

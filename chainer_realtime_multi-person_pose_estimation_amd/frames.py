@@ -69,6 +69,16 @@ def unpack_records(buf, max_persons):
     return out
 
 
+def count_persons(buf, max_persons):
+    """(sum of the exact per-frame person counts, frames whose status is OP_ERR_CAPACITY = over
+    the batched post-process caps, to be fetched with op_fetch_result) of packed records."""
+    rb = record_bytes(max_persons)
+    a = np.frombuffer(buf, np.uint8).reshape(-1, rb)
+    hdr = np.ascontiguousarray(a[:, :HDR_BYTES]).view(np.int32)  # status, n_peaks, n_persons, ...
+    ok = hdr[:, 0] == 0
+    return int(hdr[ok, 2].sum()), int((hdr[:, 0] == 3).sum())
+
+
 # ---------------------------------------------------------------- transport
 def _recv_exact(sock, n):
     chunks, got = [], 0
@@ -237,15 +247,17 @@ class RcclGather(object):
                                                                self.max_persons, int(frame_base),
                                                                int(frame_stride)), "op_comm_gather_results")
 
-    def wait(self, timeout=None):
+    def wait(self, timeout=None, raw=False):
+        """Rank 0: every rank's records of the oldest submitted step (unpacked, by frame id; or the
+        raw record bytes with raw=True); other ranks: None."""
         ct = self._ct
         p, nf, rb = ct.c_void_p(), ct.c_int32(), ct.c_int64()
         self._lib.check(self._lib.lib().op_comm_wait(self.h, float(timeout or self.timeout), ct.byref(p),
                                                      ct.byref(nf), ct.byref(rb)), "op_comm_wait")
         if not p.value:
             return None
-        raw = ct.string_at(p.value, nf.value * rb.value)
-        return unpack_records(raw, self.max_persons)
+        buf = ct.string_at(p.value, nf.value * rb.value)
+        return buf if raw else unpack_records(buf, self.max_persons)
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
