@@ -56,12 +56,8 @@ struct BigTiling {
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 4, "vmcnt literal");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  static_assert(N >= 0 && N <= 63, "vmcnt literal");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // nt (1 or 2) consecutive taps t, t+1 of one chunk for one wave: 2 channel blocks x NPB pixel
@@ -463,7 +459,11 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
 // 64 channels (4 blocks of 16) x NPX 16-pixel blocks of a raster tile; D rows are channels (4
 // consecutive per lane), columns pixels.  Halo, 4-slot weight ring (one barrier per tap pair, 2
 // taps ahead) and XCD-aware block order as conv_big_bf16x3<7,..,RASTER>.
-template <int KS, int NPX>
+// DEEP (small tiles, halo planes <= 16 KiB): a 12-slot weight ring staged 5 tap pairs ahead instead
+// of 4 slots / 1 pair.  A small tile's workgroup does little MFMA work per tap pair, so with one pair
+// of prefetch it waits on the weight fetch (L2 / HBM latency) every pair: the single-frame and
+// single-crop launches.
+template <int KS, int NPX, bool DEEP = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
   constexpr int KSQ = KS * KS;
@@ -471,11 +471,12 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
   constexpr int PLANE_W = CW * 16;
   constexpr int SLOT_W = 4 * PLANE_W;
-  constexpr int RING = 4;
+  constexpr int RING = DEEP ? 12 : 4;    // taps; even, so a pair never wraps
+  constexpr int AHEAD = RING / 2 - 1;    // tap pairs staged ahead of the one being computed
   constexpr int CAP = PG * NPX * 16;
-  // halo planes at a fixed 32-KiB stride (raster_tiling keeps nh <= 32), placed first so a lane's
-  // lo-plane read is its hi-plane address + an immediate offset; the weight ring follows
-  constexpr int HPLANE = 32 * 1024;
+  // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16), placed first so a
+  // lane's lo-plane read is its hi-plane address + an immediate offset; the weight ring follows
+  constexpr int HPLANE = (DEEP ? 16 : 32) * 1024;
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
 
   const int lin = blockIdx.x;
@@ -536,7 +537,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int n_it = cb1 * KSQP;
   const char* const zsrc = (const char*)tl.zeros + lane * 16;
   auto stage_w = [&](int it) {
-    char* dst = ring + (it % RING) * SLOT_W;
+    char* dst = ring + ((unsigned)it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
     const int c = it / KSQP, tp = it - c * KSQP;
     glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
@@ -563,8 +564,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  stage_w(cb0 * KSQP);
-  stage_w(cb0 * KSQP + 1);
+#pragma unroll
+  for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
@@ -597,18 +598,18 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     bf16x8g ah[4], al[4];
 #pragma unroll 1
     for (int t = 0; t < KSQP; t += 2, it += 2) {
-      wait_vmcnt<0>();  // W(it), W(it+1): the newest copies, issued one pair back ...
+      wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
       __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
       asm volatile("" ::: "memory");
-      stage_w(it + 2);
-      stage_w(it + 3);
+      stage_w(it + 2 * AHEAD);
+      stage_w(it + 2 * AHEAD + 1);
       // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
       // tap (zero weights) reads tap t's pixels: finite values, times zero
       const int t1 = t + 1 < KSQ ? t + 1 : t;
       const int toff0 = ((t / KS) * tl.pitch + (t - (t / KS) * KS)) * 16;
       const int toff1 = ((t1 / KS) * tl.pitch + (t1 - (t1 / KS) * KS)) * 16;
       const int toff = tsel ? toff1 : toff0;
-      const char* wsl = ring + (((unsigned)(it + tsel) & (RING - 1)) * SLOT_W) + wlane;
+      const char* wsl = ring + ((unsigned)it % RING + tsel) * SLOT_W + wlane;  // it even: no wrap
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
@@ -1419,7 +1420,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 8>,
                              (const void*)conv_m16_bf16x3<7, 6>,
                              (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
-                             (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>};
+                             (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>,
+                             (const void*)conv_m16_bf16x3<7, 5, true>, (const void*)conv_m16_bf16x3<7, 4, true>,
+                             (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>};
         for (const void* f : fns)
           OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
@@ -1428,7 +1431,11 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         set_error("conv_m16_bf16x3: halo plane over 32 KiB");
         return OP_ERR_INVALID;
       }
-      const int lds = 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes at a fixed 32-KiB stride
+      // small tiles whose halo planes fit 16 KiB take the deep weight ring (12 taps, 5 pairs ahead)
+      static const bool no_deep = getenv("OP_M16_NODEEP") && atoi(getenv("OP_M16_NODEEP")) != 0;  // A/B aid
+      const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
+      const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
+                           : 4 * 4 * 128 * 16 + 4 * 32 * 1024;   // ring + 4 halo planes (32-KiB stride)
       const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                      : (unsigned)(tl.units * tl.per_unit);
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
@@ -1436,10 +1443,22 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       switch (npx) {
         case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
         case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 5: hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 4: hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 3: hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 2: hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
+        case 5:
+          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 5, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          break;
+        case 4:
+          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 4, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          break;
+        case 3:
+          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 3, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          break;
+        case 2:
+          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 2, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g[0], g1, tl);
+          break;
         default: hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g[0], g1, tl);
       }
       if (tl.ksplit > 1) {
