@@ -122,3 +122,18 @@ def test_gather_times_out_on_a_stalled_rank():
     for p in procs:
         p.join(timeout=30)
     assert "timed out" in msg and dt < 5.0, (msg, dt)
+
+
+def test_count_persons_reads_exact_header_counts():
+    """frames.count_persons (bench.py's device-record path): exact n_persons from the headers even
+    past max_persons, zero for failed frames, over-cap frames (status 3) counted apart."""
+    F = pkg_module("frames")
+    rng = np.random.default_rng(0)
+    recs = []
+    for i in range(9):
+        k = int(rng.integers(0, 7))
+        status = 3 if i == 4 else 0
+        recs.append((i, status, 40, rng.random((k, 18, 3)), rng.random(k)))
+    buf = F.pack_records(recs, 4).tobytes()
+    want = sum(len(r[4]) for r in recs if r[1] == 0)
+    assert F.count_persons(buf, 4) == (want, 1)

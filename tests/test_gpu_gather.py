@@ -63,3 +63,26 @@ def test_rccl_gather_one_rank_double_buffered(ctx):
     finally:
         ctx.use_staged_maps(False)
         g.close()
+
+
+def test_pipelined_raw_records_count_like_fetch_results(ctx):
+    """bench.py's step loop: step k's records are collected (raw) while step k+1 runs; the exact
+    person counts of the headers equal op_fetch_results' for the same frames."""
+    F = pkg_module("frames")
+    g = F.RcclGather(ctx, F.SocketTransport(0, 1), max_persons=MAXP, timeout=30)
+    _staged(ctx, 3)
+    try:
+        ctx.run_staged()
+        ctx.synchronize()
+        want = sum(r.n_persons for _, _, r in ctx.fetch_results(0, 3))
+        ctx.run_staged()
+        g.submit(0, 3, 0, 1)
+        ctx.run_staged()               # the next step is queued before the first is collected
+        g.submit(0, 3, 3, 1)
+        persons0, over0 = F.count_persons(g.wait(raw=True), MAXP)
+        persons1, over1 = F.count_persons(g.wait(raw=True), MAXP)
+        assert want > 3 * MAXP - 1     # the golden frames hold more persons than a record carries
+        assert (persons0, over0) == (want, 0) and (persons1, over1) == (want, 0)
+    finally:
+        ctx.use_staged_maps(False)
+        g.close()
