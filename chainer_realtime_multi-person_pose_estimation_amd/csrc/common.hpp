@@ -175,6 +175,17 @@ int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, 
 int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
                             float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st);
 // planar source (c*cstride + y*sstride + x) -> planar destination, modes 1-3 (precise.hip)
+// Per scale k: the padded-size map of one frame (planar, cstride floats per channel, sstride per
+// row), cropped to sh x sw, and the host-computed cubic scales to the output size.
+struct CubicMeanArgs {
+  const float* src[OP_MAX_SCALES];
+  int64_t cstride[OP_MAX_SCALES], sstride[OP_MAX_SCALES];
+  int sh[OP_MAX_SCALES], sw[OP_MAX_SCALES];
+  double scx[OP_MAX_SCALES], scy[OP_MAX_SCALES];
+  int ns;
+};
+int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int32_t dh, int32_t dw, int32_t npaf,
+                                        int32_t nheat, hipStream_t st);
 int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t sstride, int32_t sh, int32_t sw,
                                    int32_t cn, float* dst, int32_t dh, int32_t dw, int32_t mode, float div,
                                    hipStream_t st);

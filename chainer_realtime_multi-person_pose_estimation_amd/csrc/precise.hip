@@ -156,6 +156,44 @@ int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t ss
   return OP_OK;
 }
 
+// All scales' second pass at once (pose_detector.py:461-470): for every output pixel and map
+// channel, the cubic resize of each scale's cropped padded-size map, summed in scale order and
+// divided by the scale count -- the same f32 operations, in the same order, as mode 1 / 2 / 3 of
+// resize_cubic_f32_planar, without writing and re-reading the running sum once per scale.
+// Channels 0..npaf-1 are the PAF map (its own cv2.resize call: SIMD/tail split over npaf
+// interleaved channels), npaf.. the heatmap (nheat channels).
+__global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean(CubicMeanArgs a, float* __restrict__ dst, int dh,
+                                                                    int dw, int npaf, int nheat) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y, c = blockIdx.z;
+  if (x >= dw) return;
+  const bool paf = c < npaf;
+  const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+  float sum = 0.0f;
+  for (int k = 0; k < a.ns; ++k) {
+    const CubicTap tx = cv_cubic_tap_s(x, a.scx[k]);
+    const CubicTap ty = cv_cubic_tap_s(y, a.scy[k]);
+    const float v = cv_cubic_f32(a.src[k], a.sstride[k], 1, a.sh[k], a.sw[k], c, tx, ty, x * cn + ce,
+                                 dw * cn / 4 * 4, a.cstride[k]);
+    sum = k == 0 ? v : __fadd_rn(sum, v);
+  }
+  dst[((int64_t)c * dh + y) * dw + x] = __fdiv_rn(sum, (float)a.ns);
+}
+
+int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int32_t dh, int32_t dw, int32_t npaf,
+                                        int32_t nheat, hipStream_t st) {
+  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
+    set_error("resize_cubic_f32_planar_mean: 1..OP_MAX_SCALES scales");
+    return OP_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(resize_cubic_f32_planar_mean, dim3((unsigned)((dw + 255) / 256), (unsigned)dh,
+                                                        (unsigned)(npaf + nheat)),
+                     dim3(256), 0, st, a, dst, dh, dw, npaf, nheat);
+  OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 // Generic cv2.resize(INTER_CUBIC) of a cn-channel uint8 image (row stride sstride bytes) to a
 // contiguous dh x dw x cn image (the stage-level ABI op_resize_cubic).
 __global__ __launch_bounds__(256) void resize_cubic_u8(const uint8_t* __restrict__ src, int64_t sstride, int sh, int sw,

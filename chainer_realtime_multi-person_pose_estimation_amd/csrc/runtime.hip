@@ -2297,7 +2297,7 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   const int ds = c->prm.downscale;
   const int ns = c->prm.n_scales;
   int rws[OP_MAX_SCALES], rhs[OP_MAX_SCALES], pws[OP_MAX_SCALES], phs[OP_MAX_SCALES];
-  size_t mid_max = 0;
+  size_t mid_off[OP_MAX_SCALES + 1] = {0};  // floats: every scale's padded-size maps of every frame
   for (int k = 0; k < ns; ++k) {
     const double m = c->prm.inference_scales[k] * (double)c->prm.inference_img_size / (double)(h < w ? h : w);
     rws[k] = (int)std::ceil((double)w * m);
@@ -2308,10 +2308,10 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       set_error("detect_precise: a scale gives a network input below 16 x 16");
       return OP_ERR_INVALID;
     }
-    mid_max = std::max(mid_max, (size_t)phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT) * 4);
+    mid_off[k + 1] = mid_off[k] + (size_t)n * phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT);
   }
   const int64_t fplanes = (int64_t)(OP_N_PAF + OP_N_HEAT) * h * w;  // floats per frame of psum
-  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_max, "precise_mid"));
+  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_off[ns] * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;
   for (int k = 0; k < ns; ++k) {
@@ -2344,23 +2344,34 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       paf_off = kCatPaf;
       heat_off = kCatHeat;
     }
-    const int mode = k == 0 ? 1 : (k == ns - 1 ? 3 : 2);
     for (int f = 0; f < n; ++f) {
       const float* mf = mbase + f * mframe;
-      float* sum_paf = c->d_psum + f * fplanes;
-      float* sum_heat = sum_paf + (size_t)OP_N_PAF * h * w;
       // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping),
-      // stored planar (cn, ph, pw) so the second resize reads coalesced rows
-      float* mid_paf = c->d_pmid;
-      float* mid_heat = c->d_pmid + (size_t)ph * pw * OP_N_PAF;
+      // stored planar (cn, ph, pw) so the second resize reads coalesced rows; kept for every scale
+      // and frame until the fused second pass below
       const int64_t pp = (int64_t)ph * pw;
+      float* mid_paf = c->d_pmid + mid_off[k] + (size_t)f * pp * (OP_N_PAF + OP_N_HEAT);
+      float* mid_heat = mid_paf + (size_t)pp * OP_N_PAF;
       RC(launch_resize_cubic_f32(mf + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 1, 1.0f, c->stream));
       RC(launch_resize_cubic_f32(mf + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 1, 1.0f, c->stream));
-      // :462-463 / :466-467 crop to rh x rw, cubic to h x w, running sum (mean after the last scale)
-      RC(launch_resize_cubic_f32_planar(mid_paf, pp, pw, rh, rw, OP_N_PAF, sum_paf, h, w, mode, (float)ns, c->stream));
-      RC(launch_resize_cubic_f32_planar(mid_heat, pp, pw, rh, rw, OP_N_HEAT, sum_heat, h, w, mode, (float)ns,
-                                        c->stream));
     }
+  }
+  // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
+  // order and divided by the scale count: one pass per frame over the PAF and heat planes
+  for (int f = 0; f < n; ++f) {
+    CubicMeanArgs a{};
+    a.ns = ns;
+    for (int k = 0; k < ns; ++k) {
+      const int64_t pp = (int64_t)phs[k] * pws[k];
+      a.src[k] = c->d_pmid + mid_off[k] + (size_t)f * pp * (OP_N_PAF + OP_N_HEAT);
+      a.cstride[k] = pp;
+      a.sstride[k] = pws[k];
+      a.sh[k] = rhs[k];
+      a.sw[k] = rws[k];
+      a.scx[k] = 1.0 / ((double)w / (double)rws[k]);  // cv_cubic_scale (cvcubic.hpp): OpenCV's f64 inverse scale
+      a.scy[k] = 1.0 / ((double)h / (double)rhs[k]);
+    }
+    RC(launch_resize_cubic_f32_planar_mean(a, c->d_psum + f * fplanes, h, w, OP_N_PAF, OP_N_HEAT, c->stream));
   }
   // :474-482 post-process at the original resolution: img_len = orig_w, no rescale.  With staged
   // full-resolution maps (op_stage_maps at the frame size + op_use_staged_maps) the post-process
