@@ -40,6 +40,7 @@ struct op_comm {
   int64_t rbytes[2] = {0, 0};
   int order[2] = {-1, -1};              // FIFO of outstanding slots
   bool aborted = false;
+  double timeout_s = 0.0;               // op_comm_create's per-rank timeout (init and enqueue waits)
 };
 
 namespace {
@@ -122,6 +123,7 @@ int op_comm_create(op_ctx* ctx, int32_t world, int32_t rank, const uint8_t* id, 
   g->world = world;
   g->rank = rank;
   g->device = ctx_device(ctx);
+  g->timeout_s = timeout_s;
   auto fail = [&](int rc) {
     if (g->comm) (void)ncclCommAbort(g->comm);
     if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -224,7 +226,7 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
   if (r == ncclInProgress) {
     // non-blocking communicator: the gather may still be on its way into g->stream; the root's D2H
     // copy must be enqueued behind it, so wait until RCCL reports the call complete (bounded)
-    RC(wait_for(g, 300.0, "ncclGather enqueue", [&]() -> int {
+    RC(wait_for(g, g->timeout_s, "ncclGather enqueue", [&]() -> int {
       ncclResult_t ae = ncclInProgress;
       if (ncclCommGetAsyncError(g->comm, &ae) != ncclSuccess) return -1;
       return ae == ncclSuccess ? 1 : 0;  // an error state is reported (and aborted) by wait_for

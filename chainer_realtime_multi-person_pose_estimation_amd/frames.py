@@ -23,6 +23,7 @@ import time
 import numpy as np
 
 N_JOINTS = 18
+STATUS_CAPACITY = 3  # OP_ERR_CAPACITY (include/openpose_hip.h): the frame exceeded the batched caps
 HDR_BYTES = 32  # int32 status, n_peaks, n_persons, 0; int64 frame id; 8 pad
 
 
@@ -76,7 +77,7 @@ def count_persons(buf, max_persons):
     a = np.frombuffer(buf, np.uint8).reshape(-1, rb)
     hdr = np.ascontiguousarray(a[:, :HDR_BYTES]).view(np.int32)  # status, n_peaks, n_persons, ...
     ok = hdr[:, 0] == 0
-    return int(hdr[ok, 2].sum()), int((hdr[:, 0] == 3).sum())
+    return int(hdr[ok, 2].sum()), int((hdr[:, 0] == STATUS_CAPACITY).sum())
 
 
 # ---------------------------------------------------------------- transport
