@@ -58,7 +58,10 @@ static int guard_check(const char* where) {
   std::lock_guard<std::mutex> lk(g_band_mu);
   std::vector<unsigned char> h(g_guard);
   for (auto& g : g_bands) {
-    if (hipMemcpy(h.data(), g.p, g_guard, hipMemcpyDeviceToHost) != hipSuccess) continue;
+    if (hipMemcpy(h.data(), g.p, g_guard, hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();  // a band of a buffer freed without guard_forget: not a kernel fault,
+      continue;                 // and the sticky error must not surface at the next launch check
+    }
     for (size_t i = 0; i < g_guard; ++i)
       if (h[i] != 0xA5) {
         char msg[256];
@@ -1225,6 +1228,7 @@ int op_destroy(op_ctx* c) {
   guard_forget(c->d_frames, c->frames_bytes + g_guard);
   guard_forget(c->d_maps, c->maps_bytes + g_guard);
   guard_forget(c->d_scratch, c->scratch_bytes + g_guard);
+  guard_forget(c->d_fmaps, c->fmaps_bytes + g_guard);
   if (c->post_arena) hipFree(c->post_arena);
   if (c->d_frames) hipFree(c->d_frames);
   if (c->d_maps) hipFree(c->d_maps);
