@@ -490,3 +490,22 @@ def test_cli_on_person_png_draws_the_detected_poses(tmp_path, pkg, rand_weights)
     got = D.read_bgr(out)
     assert got.shape == (584, 584, 3)
     assert np.array_equal(got, want)
+
+
+def test_profile_counts_every_7x7_launch_with_joined_events(ctx, lib):
+    """bench.py's roofline timing: Mconv1..Mconv5 of a stage share one event pair (prof_join), yet
+    the class still counts 25 launches and the algorithmic FLOPs of all of them per forward."""
+    ctx.stage_frames(np.zeros((2, 368, 368, 3), np.uint8))  # net 368 x 368, maps 46 x 46
+    ctx.profile_classes(["conv7x7"])
+    ctx.profile(True)
+    ctx.profile_reset()
+    try:
+        for _ in range(2):
+            ctx.run_staged()
+        ctx.synchronize()
+        ms, n, fl, by = ctx.profile_read()["conv7x7"]
+    finally:
+        ctx.profile(False)
+    assert n == 2 * 25 and ms > 0.0
+    # 2 runs x 2 frames x 5 stages x 2 branches x 2 FLOP x 49 taps x 128 outputs x (185 + 4 x 128) inputs x 46^2
+    assert fl == 2 * 2 * 5 * 2 * 2 * 49 * 128 * (185 + 4 * 128) * 46 * 46
