@@ -26,39 +26,10 @@
 #include <cstdlib>
 #include <vector>
 
-#include "common.hpp"
+#include "conv_big.hpp"
 
 namespace op {
 
-typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
-typedef unsigned short u16x4g __attribute__((ext_vector_type(4)));
-
-#define LDS_PTR_G(p) ((__attribute__((address_space(3))) void*)(p))
-
-struct BigTiling {
-  int32_t tr, tc;            // tile rows x cols
-  int32_t tiles_y, tiles_x;  // tiles per frame
-  int32_t pitch;             // LDS halo row pitch in 16-B slots (halo_pitch)
-  int32_t hrows;             // tr + ks - 1
-  int32_t nh;                // 1-KiB halo pieces per plane
-  int32_t units;             // weight sets = groups x channel tiles
-  int32_t co_tiles;          // channel tiles per group
-  int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
-  int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
-  int32_t hw, total;         // raster tiles: pixels per frame, pixels of the batch
-  int32_t fa_tiles;          // > 0 (conv_m16): raster tiles aligned to frames, fa_tiles per frame
-  int32_t per_xcd;           // > 0: pixel-major XCD order (conv_m16k): XCD x runs pixel tiles
-                             // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
-  int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
-  float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
-  const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 63, "vmcnt literal");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 // nt (1 or 2) consecutive taps t, t+1 of one chunk for one wave: 2 channel blocks x NPB pixel
 // blocks.  The B fragments are software-pipelined one block ahead (also into the next tap), so
@@ -406,275 +377,6 @@ __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : 2) void conv_big_bf16x
   }
 }
 
-// Epilogue of the 16x16x32 kernels: a lane holds 4 consecutive output channels c..c+3 of one pixel
-// (D rows = channels, row kg = lane / 16), so rows kg and kg ^ 1 together hold one 8-channel group
-// whose split record is [hi c..c+7 (16 B)][lo c..c+7 (16 B)].  own = this lane's {hi, hi, lo, lo}
-// dwords; w = the same after v_permlane16_swap (odd rows of the hi operand <-> even rows of the lo
-// operand): the even row then holds the group's 16 hi bytes and the odd row its 16 lo bytes, so one
-// 16-B store per lane replaces two 8-B stores.  Every lane of the wave must execute this.
-__device__ __forceinline__ void split_pair_swap(const floatx4& acc, const floatx4& bv, int relu, floatx4& v,
-                                                uint32_t own[4], uint32_t w[4]) {
-  unsigned short hb[4], lb[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float fv = acc[e] + bv[e];
-    if (relu) fv = fv > 0.0f ? fv : 0.0f;
-    v[e] = fv;
-    const __bf16 h16 = (__bf16)fv;
-    const __bf16 l16v = (__bf16)(fv - (float)h16);
-    hb[e] = __builtin_bit_cast(unsigned short, h16);
-    lb[e] = __builtin_bit_cast(unsigned short, l16v);
-  }
-  own[0] = hb[0] | ((uint32_t)hb[1] << 16);
-  own[1] = hb[2] | ((uint32_t)hb[3] << 16);
-  own[2] = lb[0] | ((uint32_t)lb[1] << 16);
-  own[3] = lb[2] | ((uint32_t)lb[3] << 16);
-  const auto r0 = __builtin_amdgcn_permlane16_swap(own[0], own[2], false, false);
-  const auto r1 = __builtin_amdgcn_permlane16_swap(own[1], own[3], false, false);
-  w[0] = r0[0];
-  w[1] = r1[0];
-  w[2] = r0[1];
-  w[3] = r1[1];
-}
-
-// Store one lane's part of an 8-channel group (see split_pair_swap): one 16-B store when the whole
-// group is stored, else (a group cut by cout_store) this lane's own two 8-B pieces.
-__device__ __forceinline__ void store_split_group(char* optr, int co, int kg, int cout_store, const uint32_t own[4],
-                                                  const uint32_t w[4]) {
-  char* gp = optr + (co >> 3) * 32;
-  if ((co | 7) < cout_store) {
-    *(uint4*)(gp + (kg & 1) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {
-    *(uint2*)(gp + (co & 7) * 2) = make_uint2(own[0], own[1]);
-    *(uint2*)(gp + 16 + (co & 7) * 2) = make_uint2(own[2], own[3]);
-  }
-}
-
-// ---- 7x7 on v_mfma_f32_16x16x32_bf16, raster tiles (the default 7x7 kernel) ----
-// K = 32 of the 16x16x32 form is fed with a tap PAIR of one 16-channel chunk: lane group
-// g = lane / 16 holds k = 8g..8g+7 = tap t + g/2, channel half g%2, so halo and weight ring keep
-// the layout above (the odd last tap pairs with zero weights).  Under the power limit this MFMA
-// sustains ~15 % more FLOP/s than 32x32x16 on random data (tools/micro/mfma_peak.hip); in the
-// network it runs the 7x7 layers 6.7 % faster per frame than conv_big_bf16x3<7,..,RASTER>.  Wave:
-// 64 channels (4 blocks of 16) x NPX 16-pixel blocks of a raster tile; D rows are channels (4
-// consecutive per lane), columns pixels.  Halo, 4-slot weight ring (one barrier per tap pair, 2
-// taps ahead) and XCD-aware block order as conv_big_bf16x3<7,..,RASTER>.
-// DEEP (small tiles, halo planes <= 16 KiB): a 12-slot weight ring staged 5 tap pairs ahead instead
-// of 4 slots / 1 pair.  A small tile's workgroup does little MFMA work per tap pair, so with one pair
-// of prefetch it waits on the weight fetch (L2 / HBM latency) every pair: the single-frame and
-// single-crop launches.
-template <int KS, int NPX, bool DEEP = false>
-__global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
-                                                          BigTiling tl) {
-  constexpr int KSQ = KS * KS;
-  constexpr int R = KS / 2;
-  constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
-  constexpr int PLANE_W = CW * 16;
-  constexpr int SLOT_W = 4 * PLANE_W;
-  constexpr int RING = DEEP ? 12 : 4;    // taps; even, so a pair never wraps
-  constexpr int AHEAD = RING / 2 - 1;    // tap pairs staged ahead of the one being computed
-  constexpr int CAP = PG * NPX * 16;
-  // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16), placed first so a
-  // lane's lo-plane read is its hi-plane address + an immediate offset; the weight ring follows
-  constexpr int HPLANE = (DEEP ? 16 : 32) * 1024;
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
-
-  const int lin = blockIdx.x;
-  int unit, widx;
-  if (tl.xpu) {
-    const int xcd = lin & 7, slot = lin >> 3;
-    unit = xcd / tl.xpu;
-    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
-  } else {
-    unit = lin / tl.per_unit;
-    widx = lin - unit * tl.per_unit;
-  }
-  if (unit >= tl.units || widx >= tl.per_unit) return;
-  const int grp = unit / tl.co_tiles;
-  const int co0 = (unit - grp * tl.co_tiles) * CW;
-  const SplitConvGroup g = grp == 0 ? g0 : g1;
-  if (co0 >= g.cop) return;
-  int P0, P1;
-  if (tl.fa_tiles) {  // frame-aligned raster tiles (wide maps): one frame per tile, last one partial
-    const int f = widx / tl.fa_tiles;
-    P0 = f * tl.hw + (widx - f * tl.fa_tiles) * CAP;
-    P1 = min(P0 + CAP, (f + 1) * tl.hw) - 1;
-  } else {
-    P0 = widx * CAP;
-    P1 = min(P0 + CAP, tl.total) - 1;
-  }
-  const int frame = P0 / tl.hw;
-  const int y0 = (P0 - frame * tl.hw) / s.w;
-  const int fb = P1 / tl.hw;
-  const int rowsA = fb != frame ? s.h - y0 + 2 * R : (1 << 30);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ch = wave / PG, pg = wave % PG;
-  const int l16 = lane & 15, kg = lane >> 4;  // k group: tap t + kg/2, channel half kg%2
-  const int tsel = kg >> 1, khalf = kg & 1;
-  char* const halo = lds;
-  char* const ring = lds + 4 * HPLANE;
-  const int wp_in = s.w + 2 * s.pin;
-  const int hp_in = s.h + 2 * s.pin;
-  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
-  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
-  const char* const fbase_b = (const char*)g.in + (int64_t)fb * hp_in * wp_in * pix_bytes;
-
-  // weights: wave w copies piece w: plane w / 2, channels co0 + 64*(w % 2) + 0..63
-  const int64_t wplane = (int64_t)g.cop * 16;
-  const int64_t wstep = 4 * wplane;
-  const char* const wsrc = (const char*)g.w + (wave / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
-  const int wdst = (wave / 2) * PLANE_W + (wave % 2) * 1024;
-  // split-K (tl.ksplit > 1): this workgroup runs input chunks [cb0, cb1)
-  const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
-  const int split = nsplit > 1 ? (int)blockIdx.y : 0;
-  const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
-  // ring index it = chunk * KSQP + tap over an even tap count per chunk: the odd 49th tap pairs with
-  // a padding tap whose weights are staged from device zeros, so every pair is a full K = 32 step
-  // (no per-pair masking of the A fragments)
-  constexpr int KSQP = KSQ + (KSQ & 1);
-  const int n_it = cb1 * KSQP;
-  const char* const zsrc = (const char*)tl.zeros + lane * 16;
-  auto stage_w = [&](int it) {
-    char* dst = ring + ((unsigned)it % RING) * SLOT_W;
-    if (it >= n_it) it = n_it - 1;
-    const int c = it / KSQP, tp = it - c * KSQP;
-    glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
-  };
-
-  // this lane's pixel of each block -> byte offset of its halo slot in its hi plane (2 khalf), so
-  // a B fragment address is qb[pb] + the tap's offset: one VALU add per block
-  int qb[NPX];
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    int q = 0;
-    if (P <= P1) {
-      const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
-      const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
-      q = (f == frame ? y - y0 : rowsA + y) * tl.pitch + x;
-    }
-    qb[pb] = (2 * khalf) * HPLANE + q * 16;
-  }
-
-  floatx4 acc[4][NPX];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
-  const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
-  const int h_plane = wave & 3, h_i0 = wave >> 2;
-  const int h_sl0 = h_i0 * 64 + lane;
-  const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
-  int it = cb0 * KSQP;
-  for (int c = cb0; c < cb1; ++c) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    {
-      const char* src0 = fbase + c * 64 + h_plane * 16;
-      const char* src0_b = fbase_b + c * 64 + h_plane * 16;
-      int hr = h_r0, hc = h_c0;
-      char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
-      for (int i = h_i0; i < tl.nh; i += 2) {
-        const bool in_a = hr < rowsA;
-        const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
-        const int xx = min(hc - R + s.pin, wp_in - 1);
-        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
-        dst += 2 * 1024;
-        hc += 2 * 64;
-        while (hc >= tl.pitch) {
-          hc -= tl.pitch;
-          ++hr;
-        }
-      }
-    }
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    bf16x8g ah[4], al[4];
-#pragma unroll 1
-    for (int t = 0; t < KSQP; t += 2, it += 2) {
-      wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
-      __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
-      asm volatile("" ::: "memory");
-      stage_w(it + 2 * AHEAD);
-      stage_w(it + 2 * AHEAD + 1);
-      // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
-      // tap (zero weights) reads tap t's pixels: finite values, times zero
-      const int t1 = t + 1 < KSQ ? t + 1 : t;
-      const int toff0 = ((t / KS) * tl.pitch + (t - (t / KS) * KS)) * 16;
-      const int toff1 = ((t1 / KS) * tl.pitch + (t1 - (t1 / KS) * KS)) * 16;
-      const int toff = tsel ? toff1 : toff0;
-      const char* wsl = ring + ((unsigned)it % RING + tsel) * SLOT_W + wlane;  // it even: no wrap
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
-        al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
-      }
-      bf16x8g bh[2], bl[2];
-      bh[0] = *(const bf16x8g*)(halo + qb[0] + toff);
-      bl[0] = *(const bf16x8g*)(halo + qb[0] + toff + HPLANE);
-#pragma unroll
-      for (int pb = 0; pb < NPX; ++pb) {
-        const int cur = pb & 1;
-        if (pb + 1 < NPX) {
-          const char* bp = halo + qb[pb + 1] + toff;
-          bh[cur ^ 1] = *(const bf16x8g*)bp;
-          bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-        }
-      }
-    }
-  }
-  wait_vmcnt<0>();
-
-  if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
-    const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
-    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) {
-      const int P = P0 + (pg * NPX + pb) * 16 + l16;
-      if (P > P1) continue;
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-        if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
-      }
-    }
-    return;
-  }
-  const int wp_out = s.w + 2 * s.pout;
-  const int hp_out = s.h + 2 * s.pout;
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    const int f = P / tl.hw, pp = P - f * tl.hw;
-    const int y = pp / s.w, x = pp - y * s.w;
-    char* optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
-    float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-      floatx4 v;
-      uint32_t own[4], w[4];
-      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
-                      v, own, w);
-      if (P > P1 || co >= g.cout_store) continue;
-      store_split_group(optr, co, kg, g.cout_store, own, w);
-      if (o32) *(floatx4*)(o32 + co) = v;
-    }
-  }
-}
 
 // Device zeros per HIP device (the 7x7 padding tap's weights), allocated outside any stream capture
 // by conv_big_device_init() when a context is created.
@@ -1391,7 +1093,6 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         return OP_ERR_STATE;
       }
       *taken = 1;
-      static bool attr = false;
       // Split-K for launches that still leave most CUs idle (one frame, one crop): the input
       // chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce), since a
       // workgroup's time is mostly its per-chunk, per-tap-pair work, not its pixel count
@@ -1416,51 +1117,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
           }
         }
       }
-      if (!attr) {
-        const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 8>,
-                             (const void*)conv_m16_bf16x3<7, 6>,
-                             (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
-                             (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>,
-                             (const void*)conv_m16_bf16x3<7, 5, true>, (const void*)conv_m16_bf16x3<7, 4, true>,
-                             (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>};
-        for (const void* f : fns)
-          OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-      }
-      if (tl.nh > 32) {
-        set_error("conv_m16_bf16x3: halo plane over 32 KiB");
-        return OP_ERR_INVALID;
-      }
-      // small tiles whose halo planes fit 16 KiB take the deep weight ring (12 taps, 5 pairs ahead)
-      static const bool no_deep = getenv("OP_M16_NODEEP") && atoi(getenv("OP_M16_NODEEP")) != 0;  // A/B aid
-      const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
-      const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
-                           : 4 * 4 * 128 * 16 + 4 * 32 * 1024;   // ring + 4 halo planes (32-KiB stride)
-      const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
-                                     : (unsigned)(tl.units * tl.per_unit);
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
-      const dim3 grid(blocks, (unsigned)tl.ksplit);
-      switch (npx) {
-        case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g[0], g1, tl); break;
-        case 5:
-          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 5, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          break;
-        case 4:
-          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 4, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          break;
-        case 3:
-          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 3, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          break;
-        case 2:
-          if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 2, true>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          else hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-          break;
-        default: hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g[0], g1, tl);
-      }
+      const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
+      if (rc != OP_OK) return rc;
       if (tl.ksplit > 1) {
         OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
         const int64_t items = (int64_t)tl.total * (cop_max / 4);
