@@ -1,6 +1,6 @@
 // Device helpers and tiling record shared by the halo-tiled conv kernels (conv_big.hip) and the
 // 7x7 raster-tile kernel (conv_m16.hip, its own translation unit so it can take its own LLVM
-// scheduler flags: Makefile M16_FLAGS).
+// scheduler flags: Makefile FLAGS_conv_m16).
 #pragma once
 #include "common.hpp"
 

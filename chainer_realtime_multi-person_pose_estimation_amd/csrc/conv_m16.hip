@@ -1,5 +1,5 @@
 // 7x7 stage convs on v_mfma_f32_16x16x32_bf16 (the default 7x7 kernel; see conv_big.hip for the
-// shared halo / weight-ring scheme).  Own translation unit: built with the Makefile's M16_FLAGS.
+// shared halo / weight-ring scheme).  Own translation unit: built with the Makefile's FLAGS_conv_m16.
 #include "conv_big.hpp"
 
 namespace op {
