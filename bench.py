@@ -16,6 +16,7 @@ Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for every field.
 import argparse
 import json
 import os
+import re
 import statistics
 import sys
 import time
@@ -115,9 +116,12 @@ def committed_traffic(kernel, batch, precision, halo_mode):
     tools/summarize_profile.py) taken on this exact workload; (None, None) when none matches."""
     import glob
     best = None
+    def age(q):  # tags r<round><letters>: r02ad follows r02z follows r02a
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(q))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(q))
+
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")) +
-                   glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic.json")),
-                   key=lambda q: os.path.relpath(q, os.path.join(REPO, "profiles")))
+                   glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic.json")), key=age)
     for p in paths:
         try:
             d = json.load(open(p))
