@@ -230,249 +230,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
 }
 
-
-// ---- 7x7 in channel-half passes: the next chunk's halo streams in behind the MFMAs ----
-// Tiles, halo planes, block order, MFMA shape and epilogue as conv_m16_bf16x3, but K = 32 holds four
-// (tap, 8-channel half) slots (m16h_slot): a chunk runs half 0's taps, then the last column's taps
-// of both halves, then half 1's -- the same 25 K = 32 steps per chunk as the tap pairs.  Half 0's two
-// halo planes are idle after step 13, so the next chunk's half-0 planes load during steps 14-23, and
-// its half-1 planes during that chunk's steps 0-8: no workgroup-wide stall at a chunk boundary,
-// where conv_m16_bf16x3 reloads all four planes with every wave waiting.  At most one 1-KiB reload
-// piece per wave per step, issued after the step's weight copy and waited for one step later than
-// it (2-step weight ring, one step ahead).
-// Step schedule of conv_m16h_bf16x3: step sp of a chunk holds tap-pair slots 2 sp and 2 sp + 1
-// (lane groups 0-1 and 2-3).  Slots 0-20: half 0, taps (r, kx), (r, kx + 1) for kx = 0, 2, 4 of row
-// r; 21-27: tap (r, 6) of half 0 beside the same tap of half 1; 28-48: half 1 as 0-20; 49: zero
-// weights (reading tap (6, 6) of half 1).  The two lane groups that share ds_read_b128 bank cycles
-// (0 and 1, 2 and 3) so read either one row at offsets <= 1 slot apart or one slot in two planes
-// 64 KiB apart: no bank conflicts.  Group g of the pair -> (ky, kx, channel half); true = zeros.
-__device__ __forceinline__ bool m16h_slot(int sp, int g, int& ky, int& kx, int& kh) {
-  const int pidx = 2 * sp + (g >> 1), e = g & 1;
-  if (pidx < 21 || (pidx >= 28 && pidx < 49)) {
-    const int q = pidx < 21 ? pidx : pidx - 28;
-    ky = q / 3;
-    kx = 2 * (q - ky * 3) + e;
-    kh = pidx < 21 ? 0 : 1;
-    return false;
-  }
-  if (pidx < 28) {
-    ky = pidx - 21;
-    kx = 6;
-    kh = e;
-    return false;
-  }
-  ky = 6;
-  kx = 6;
-  kh = 1;
-  return true;
-}
-
-template <int NPX>
-__global__ __launch_bounds__(512, 1) void conv_m16h_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
-                                                           BigTiling tl) {
-  constexpr int KS = 7, KSQ = KS * KS, R = KS / 2;
-  constexpr int CW = 128, PG = 4;   // 2 channel halves x 4 pixel groups = 8 waves
-  constexpr int PLANE_W = CW * 16;  // 128 output channels x 8 bf16 of one k group
-  constexpr int SLOT_W = 8 * PLANE_W;  // one step: 4 lane groups x hi/lo
-  constexpr int NS = 25;               // steps per chunk (m16h_slot)
-  constexpr int CAP = PG * NPX * 16;
-  constexpr int HPLANE = 32 * 1024;
-  extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring: 2 steps]
-
-  const int lin = blockIdx.x;
-  int unit, widx;
-  if (tl.xpu) {
-    const int xcd = lin & 7, slot = lin >> 3;
-    unit = xcd / tl.xpu;
-    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
-  } else {
-    unit = lin / tl.per_unit;
-    widx = lin - unit * tl.per_unit;
-  }
-  if (unit >= tl.units || widx >= tl.per_unit) return;
-  const int grp = unit / tl.co_tiles;
-  const int co0 = (unit - grp * tl.co_tiles) * CW;
-  const SplitConvGroup g = grp == 0 ? g0 : g1;
-  if (co0 >= g.cop) return;
-  int P0, P1;
-  if (tl.fa_tiles) {  // frame-aligned raster tiles (wide maps): one frame per tile, last one partial
-    const int f = widx / tl.fa_tiles;
-    P0 = f * tl.hw + (widx - f * tl.fa_tiles) * CAP;
-    P1 = min(P0 + CAP, (f + 1) * tl.hw) - 1;
-  } else {
-    P0 = widx * CAP;
-    P1 = min(P0 + CAP, tl.total) - 1;
-  }
-  const int frame = P0 / tl.hw;
-  const int y0 = (P0 - frame * tl.hw) / s.w;
-  const int fb = P1 / tl.hw;
-  const int rowsA = fb != frame ? s.h - y0 + 2 * R : (1 << 30);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ch = wave / PG, pg = wave % PG;
-  const int l16 = lane & 15, kg = lane >> 4;  // k group: tap 4s + kg of one channel half
-  char* const halo = lds;
-  char* const ring = lds + 4 * HPLANE;
-  const int wp_in = s.w + 2 * s.pin;
-  const int hp_in = s.h + 2 * s.pin;
-  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
-  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
-  const char* const fbase_b = (const char*)g.in + (int64_t)fb * hp_in * wp_in * pix_bytes;
-
-
-  // weights: wave w copies lane group w / 2's hi (w even) or lo plane, both 64-channel halves
-  const int64_t wplane = (int64_t)g.cop * 16;
-  const int64_t wstep = 4 * wplane;
-  const int sg = wave >> 1, shl = wave & 1;
-  const char* const wsrc = (const char*)g.w + shl * wplane + ((int64_t)co0 + lane) * 16;
-  const int wdst = sg * 2 * PLANE_W + shl * PLANE_W;
-  const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
-  const int split = nsplit > 1 ? (int)blockIdx.y : 0;
-  const int cb0 = split * (s.c16 / nsplit), cb1 = cb0 + s.c16 / nsplit;
-  const int n_st = cb1 * NS;
-  const char* const zsrc = (const char*)tl.zeros + lane * 16;
-  auto stage_w = [&](int st) {
-    char* dst = ring + (st & 1) * SLOT_W + wdst;
-    if (st >= n_st) st = n_st - 1;
-    const int c = st / NS, sp = st - c * NS;
-    int ky, kx, kh;
-    const bool zero = m16h_slot(sp, sg, ky, kx, kh);
-    const char* src = wsrc + (int64_t)(c * KSQ + ky * KS + kx) * wstep + 2 * kh * wplane;
-    glds16(zero ? (const void*)zsrc : (const void*)src, dst);
-    glds16(zero ? (const void*)zsrc : (const void*)(src + 64 * 16), dst + 1024);
-  };
-  // chunk c's half-kh halo planes, piece j (plane 2 kh + j % 2, 1-KiB piece j / 2)
-  auto reload = [&](int c, int kh, int j) {
-    const int i = j >> 1, p = 2 * kh + (j & 1);
-    const int sl = i * 64 + lane;
-    const int hr = sl / tl.pitch, hc = sl - (sl / tl.pitch) * tl.pitch;
-    const bool in_a = hr < rowsA;
-    const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
-    const int xx = min(hc - R + s.pin, wp_in - 1);
-    glds16((const void*)((in_a ? fbase : fbase_b) + c * 64 + p * 16 + (int64_t)(yy * wp_in + xx) * pix_bytes),
-           halo + p * HPLANE + i * 1024);
-  };
-
-  // this lane's pixel of each block -> byte offset of its halo slot within a plane
-  int qb[NPX];
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    int q = 0;
-    if (P <= P1) {
-      const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
-      const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
-      q = (f == frame ? y - y0 : rowsA + y) * tl.pitch + x;
-    }
-    qb[pb] = q * 16;
-  }
-
-  floatx4 acc[4][NPX];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  stage_w(cb0 * NS);
-  for (int kh = 0; kh < 2; ++kh)
-    for (int j = wave; j < 2 * tl.nh; j += 8) reload(cb0, kh, j);
-  const int wlane = kg * 2 * PLANE_W + (ch * 64 + l16) * 16;  // A: channel ch*64 + cb*16 + l16
-  bf16x8g ah[4], al[4];
-  bool r_out = false;  // this wave issued a reload piece in the previous step (after its weights)
-  for (int c = cb0; c < cb1; ++c) {
-#pragma unroll 1
-    for (int sp = 0; sp < NS; ++sp) {
-      const int st = c * NS + sp;
-      // this step's weights (issued a step back) landed; the previous step's reload piece, issued
-      // after them, may still be in flight: it is first read two steps later
-      if (r_out) wait_vmcnt<1>();
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();  // ... for every wave; the other ring slot is free
-      asm volatile("" ::: "memory");
-      stage_w(st + 1);
-      // reload windows end a step early, so every piece has landed at the step that reads it
-      int rj = -1, rc = c, rkh = 1;
-      if (sp < 9 && c > cb0) rj = sp * 8 + wave;  // half 1 of this chunk (first read at step 10)
-      else if (sp >= 14 && sp < 24 && c + 1 < cb1) {
-        rj = (sp - 14) * 8 + wave;  // half 0 of the next chunk (last read of this one at step 13)
-        rc = c + 1;
-        rkh = 0;
-      }
-      r_out = rj >= 0 && rj < 2 * tl.nh;
-      if (r_out) reload(rc, rkh, rj);
-      // this lane group's tap and channel half (the zero slot reads a loaded plane: finite values,
-      // times zero)
-      int ky, kx, kh;
-      (void)m16h_slot(sp, kg, ky, kx, kh);
-      const int bo = kh * 2 * HPLANE + (ky * tl.pitch + kx) * 16;
-      const char* wsl = ring + (st & 1) * SLOT_W + wlane;
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
-        al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
-      }
-      bf16x8g bh[2], bl[2];
-      bh[0] = *(const bf16x8g*)(halo + qb[0] + bo);
-      bl[0] = *(const bf16x8g*)(halo + qb[0] + bo + HPLANE);
-#pragma unroll
-      for (int pb = 0; pb < NPX; ++pb) {
-        const int cur = pb & 1;
-        if (pb + 1 < NPX) {
-          const char* bp = halo + qb[pb + 1] + bo;
-          bh[cur ^ 1] = *(const bf16x8g*)bp;
-          bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-        }
-      }
-    }
-  }
-  wait_vmcnt<0>();
-
-  if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
-    const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
-    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) {
-      const int P = P0 + (pg * NPX + pb) * 16 + l16;
-      if (P > P1) continue;
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-        if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
-      }
-    }
-    return;
-  }
-  const int wp_out = s.w + 2 * s.pout;
-  const int hp_out = s.h + 2 * s.pout;
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    const int f = P / tl.hw, pp = P - f * tl.hw;
-    const int y = pp / s.w, x = pp - y * s.w;
-    char* optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
-    float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-      floatx4 v;
-      uint32_t own[4], w[4];
-      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
-                      v, own, w);
-      if (P > P1 || co >= g.cout_store) continue;
-      store_split_group(optr, co, kg, g.cout_store, own, w);
-      if (o32) *(floatx4*)(o32 + co) = v;
-    }
-  }
-}
-
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl) {
   static bool attr = false;
@@ -482,9 +239,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
                          (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>,
                          (const void*)conv_m16_bf16x3<7, 5, true>, (const void*)conv_m16_bf16x3<7, 4, true>,
-                         (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>,
-                         (const void*)conv_m16h_bf16x3<10>, (const void*)conv_m16h_bf16x3<8>,
-                         (const void*)conv_m16h_bf16x3<6>};
+                         (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -501,16 +256,6 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
-  // the large tiles run in channel-half passes (the next chunk's halo loads behind the MFMAs)
-  static const bool no_kh = getenv("OP_M16_KHPASS") && atoi(getenv("OP_M16_KHPASS")) == 0;  // A/B aid
-  if (!deep && !no_kh && npx >= 6) {
-    switch (npx) {
-      case 8: hipLaunchKernelGGL((conv_m16h_bf16x3<8>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-      case 6: hipLaunchKernelGGL((conv_m16h_bf16x3<6>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-      default: hipLaunchKernelGGL((conv_m16h_bf16x3<10>), grid, dim3(512), lds, st, s, g0, g1, tl);
-    }
-    return OP_OK;
-  }
   switch (npx) {
     case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
     case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
