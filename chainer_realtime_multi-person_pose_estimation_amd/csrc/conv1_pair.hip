@@ -12,7 +12,9 @@
 //    g = chunk g/2, channel half g%2; products hi*hi + hi*lo + lo*hi), A fragments read from L2
 //    one step ahead;
 //  * pools 2x2 in the epilogue (rows = blocks b, b+2; columns = lanes l, l^1) into P1.
-// Waves: 4, wave w = 64 channels x the tile's rows 2w, 2w+1 (4 blocks of 16 px).  LDS 48 KiB:
+// Waves: 4, wave w = kP1CoW (32) channels x 16 / (4 / kP1Cg) (8) blocks of 16 px (tile rows
+// 4 (w / 2) .. + 3): a wave's per-step A fragments (read from L2) feed 8 pixel blocks, where 64
+// channels x 4 blocks read every A fragment in all four waves (conv1_pair -2.8 %; 16 x 16: +1.4 %).  LDS 48 KiB:
 // three workgroups per CU, so one's conv1_1 (VALU) phase overlaps the others' MFMA phases.
 #include "common.hpp"
 #include "cvlinear.hpp"
@@ -31,6 +33,13 @@ constexpr int kP1Slots = kP1HR * kP1HC;            // 340
 // spans two planes (k-halves), and with a 64-B plane offset their 16-B slots collided (2-way)
 constexpr int kP1Plane = (kP1Slots * 16 + 255) / 256 * 256;  // (no measurable change in an A/B)
 constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
+#ifndef C1P_COW
+#define C1P_COW 32
+#endif
+constexpr int kP1CoW = C1P_COW;             // conv1_2 output channels per wave (16, 32 or 64)
+constexpr int kP1Ncb = kP1CoW / 16;         // 16-channel MFMA blocks per wave
+constexpr int kP1Cg = 64 / kP1CoW;          // channel groups over the 4 waves
+constexpr int kP1Npb = 16 / (4 / kP1Cg);    // 16-px blocks per wave (the tile has 16)
 
 __device__ __forceinline__ float p1_recon(float v) {
   const __bf16 h = (__bf16)v;
@@ -80,33 +89,34 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
     for (int c = 0; c < 3; ++c) inw[c * kP1IR * kP1IC + i] = v[c];
   }
 
+  const int cs = wave % kP1Cg, ph = wave / kP1Cg;  // channel group, pixel group of this wave
   // A fragments (conv1_2 weights, split layout [c16][tap][plane][64][8]) of step (half, tap)
-  auto load_a = [&](int half, int t, bf16x8p(&ah)[4], bf16x8p(&al)[4]) {
+  auto load_a = [&](int half, int t, bf16x8p(&ah)[kP1Ncb], bf16x8p(&al)[kP1Ncb]) {
     const int c16 = 2 * half + csel;
-    const char* base = w12 + ((int64_t)((c16 * 9 + t) * 4 + 2 * khalf) * 64 + l16) * 16;
+    const char* base = w12 + ((int64_t)((c16 * 9 + t) * 4 + 2 * khalf) * 64 + kP1CoW * cs + l16) * 16;
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
+    for (int cb = 0; cb < kP1Ncb; ++cb) {
       ah[cb] = *(const bf16x8p*)(base + cb * 256);
       al[cb] = *(const bf16x8p*)(base + 64 * 16 + cb * 256);
     }
   };
 
-  floatx4 acc[4][4];
+  floatx4 acc[kP1Ncb][kP1Npb];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
+  for (int cb = 0; cb < kP1Ncb; ++cb)
 #pragma unroll
-    for (int pb = 0; pb < 4; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int pb = 0; pb < kP1Npb; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // this lane's halo slot for its 4 pixel blocks (block b = 4w + pb: row b/2, cols (b%2)*16 + l16)
-  int q[4];
+  // this lane's halo slot for its pixel blocks (block b = kP1Npb ph + pb: row b/2, cols (b%2)*16 + l16)
+  int q[kP1Npb];
 #pragma unroll
-  for (int pb = 0; pb < 4; ++pb) {
-    const int b = 4 * wave + pb;
+  for (int pb = 0; pb < kP1Npb; ++pb) {
+    const int b = kP1Npb * ph + pb;
     q[pb] = (b >> 1) * kP1HC + (b & 1) * 16 + l16;
   }
   const char* const bplane = halo + (csel * 4 + 2 * khalf) * kP1Plane;
 
-  bf16x8p ah[4], al[4];
+  bf16x8p ah[kP1Ncb], al[kP1Ncb];
   load_a(0, 0, ah, al);
   for (int half = 0; half < 2; ++half) {
     __syncthreads();  // input window staged / the previous half's MFMAs are done with the halo
@@ -169,9 +179,9 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
     // ---- conv1_2, the 9 taps of this half: K = 32 channels per step ----
 #pragma unroll 1
     for (int t = 0; t < 9; ++t) {
-      bf16x8p ch_[4], cl_[4];
+      bf16x8p ch_[kP1Ncb], cl_[kP1Ncb];
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
+      for (int cb = 0; cb < kP1Ncb; ++cb) {
         ch_[cb] = ah[cb];
         cl_[cb] = al[cb];
       }
@@ -179,12 +189,12 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
       else if (half == 0) load_a(1, 0, ah, al);
       const int toff = (t / 3) * kP1HC + t % 3;
 #pragma unroll
-      for (int pb = 0; pb < 4; ++pb) {
+      for (int pb = 0; pb < kP1Npb; ++pb) {
         const char* bp = bplane + (q[pb] + toff) * 16;
         const bf16x8p bh = *(const bf16x8p*)bp;
         const bf16x8p bl = *(const bf16x8p*)(bp + kP1Plane);
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
+        for (int cb = 0; cb < kP1Ncb; ++cb) {
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ch_[cb], bh, acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ch_[cb], bl, acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cl_[cb], bh, acc[cb][pb], 0, 0, 0);
@@ -197,15 +207,16 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
   const int wp_out = w / 2 + 2 * pout;
   const int hp_out = h / 2 + 2 * pout;
 #pragma unroll
-  for (int pb = 0; pb < 2; ++pb) {  // blocks pb (row 2w) and pb + 2 (row 2w + 1)
-    const int b = 4 * wave + pb;
+  for (int pb = 0; pb < kP1Npb; ++pb) {  // blocks pb (row 2i) and pb + 2 (row 2i + 1)
+    if (pb & 2) continue;
+    const int b = kP1Npb * ph + pb;
     const int r = b >> 1, c = (b & 1) * 16 + l16;
     const int y = y0 + r, x = x0 + c;
     const bool store = y < h && x < w && (l16 & 1) == 0;
     char* optr = out + ((int64_t)(n * hp_out + y / 2 + pout) * wp_out + (x / 2 + pout)) * 256;
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int co = cb * 16 + 4 * kg;
+    for (int cb = 0; cb < kP1Ncb; ++cb) {
+      const int co = kP1CoW * cs + cb * 16 + 4 * kg;
       const floatx4 bv = *(const floatx4*)(b12 + co);
       u16x4p vh, vl;
 #pragma unroll
