@@ -82,6 +82,10 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
 
 // conv_m16.hip: launch conv_m16_bf16x3<7, npx, deep> on a raster tiling made by conv_big.hip (picks
 // the deep weight ring for small tiles; sets the kernels' LDS attribute on first use).
+// conv_m16k_wide.hip: launch conv_m16k_bf16x3<false, 3, 6> (4 x 48 tiles; sets its LDS attribute).
+int launch_m16k_wide(dim3 grid, int lds, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
+                     const SplitConvGroup& g1, const BigTiling& tl);
+
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl);
 
