@@ -280,6 +280,10 @@ struct op_ctx {
   // async frame uploads (op_upload_frames): a 2-slot device ring filled on copy_stream; the next
   // run waits for its slot's copy and moves it into d_frames on the compute stream
   hipStream_t copy_stream = nullptr;
+  // detect_precise: the scales with at most a quarter of the largest scale's network pixels run on
+  // this side stream, concurrently with the large ones (their launches fill a fraction of the chip)
+  hipStream_t side_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* d_ring[2] = {nullptr, nullptr};
   size_t ring_bytes[2] = {0, 0};
   hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -386,6 +390,7 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
       for (size_t i = 1; i < c->arenas.size(); ++i)
         if (c->arenas[i].used < c->arenas[lru].used) lru = i;
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      if (c->side_stream) OP_HIP_CHECK(hipStreamSynchronize(c->side_stream));  // the other stream's arenas
       guard_forget(c->arenas[lru].p, c->arenas[lru].bytes);
       OP_HIP_CHECK(hipFree(c->arenas[lru].p));
       c->arenas.erase(c->arenas.begin() + lru);
@@ -1215,6 +1220,7 @@ int op_destroy(op_ctx* c) {
   if (!c) return OP_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->side_stream) hipStreamSynchronize(c->side_stream);
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
   free_weights(c);
@@ -1247,6 +1253,13 @@ int op_destroy(op_ctx* c) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
   }
+  if (c->side_stream) {
+    (void)hipStreamSynchronize(c->side_stream);
+    splitk_ws_release(c->side_stream);
+    (void)hipStreamDestroy(c->side_stream);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (int i = 0; i < 2; ++i) {
     if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
     if (c->ev_up[i]) (void)hipEventDestroy(c->ev_up[i]);
@@ -2291,6 +2304,48 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
   return op_fetch_result(c, 0, poses, scores, cap, res);
 }
 
+// Runs a part of the enqueue on c->side_stream: enter() points c->stream at the side stream (the
+// first time, after a fork event on the compute stream, so it sees everything enqueued so far),
+// leave() points it back; join() -- also run on scope exit, so an error return leaves no side work
+// unjoined -- makes the compute stream wait for the side stream's work.
+struct SideStream {
+  op_ctx* c;
+  hipStream_t main;
+  bool forked = false, inside = false;
+  explicit SideStream(op_ctx* ctx) : c(ctx), main(ctx->stream) {}
+  int enter() {
+    if (!c->side_stream) {
+      // its own hardware queue only when the process has more than HIP's default 4 (the compute,
+      // copy and communicator streams and the null stream take those): the Python loader raises
+      // GPU_MAX_HW_QUEUES to 8
+      OP_HIP_CHECK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    if (!forked) {
+      OP_HIP_CHECK(hipEventRecord(c->ev_fork, main));
+      OP_HIP_CHECK(hipStreamWaitEvent(c->side_stream, c->ev_fork, 0));
+      forked = true;
+    }
+    c->stream = c->side_stream;
+    inside = true;
+    return OP_OK;
+  }
+  void leave() {
+    c->stream = main;
+    inside = false;
+  }
+  int join() {
+    leave();
+    if (!forked) return OP_OK;
+    forked = false;
+    OP_HIP_CHECK(hipEventRecord(c->ev_join, c->side_stream));
+    OP_HIP_CHECK(hipStreamWaitEvent(main, c->ev_join, 0));
+    return OP_OK;
+  }
+  ~SideStream() { (void)join(); }
+};
+
 // detect_precise (pose_detector.py:433-482).  Sizes follow the reference's Python arithmetic:
 // multiplier = scale * inference_img_size / min(h, w) and math.ceil(w * multiplier) in f64.
 // detect_precise (pose_detector.py:433-482) for the n frames (h x w, contiguous) at c->d_frames:
@@ -2318,8 +2373,20 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_off[ns] * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;
+  // scales with <= 1/4 of the largest scale's network pixels (0.5 and 1.0 of the default 0.5/1/1.5/2)
+  // run their forward + first map resize on the side stream, concurrently with the large scales:
+  // same kernels and operands per scale, so the maps and the scale-ordered mean are unchanged
+  static const bool overlap = !(getenv("OP_PRECISE_OVERLAP") && atoi(getenv("OP_PRECISE_OVERLAP")) == 0);
+  bool on_side[OP_MAX_SCALES] = {};
+  {
+    int64_t amax = 0;
+    for (int k = 0; k < ns; ++k) amax = std::max(amax, (int64_t)phs[k] * pws[k]);
+    for (int k = 0; k < ns; ++k) on_side[k] = overlap && ns > 1 && (int64_t)phs[k] * pws[k] * 4 <= amax;
+  }
+  SideStream side(c);
   for (int k = 0; k < ns; ++k) {
     const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
+    if (on_side[k]) RC(side.enter());
     RC(ensure_geometry(c, n, ph, pw));
     const Act& x0 = c->buf[B_X0];
     for (int f = 0; f < n; ++f)
@@ -2359,7 +2426,9 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       RC(launch_resize_cubic_f32(mf + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 1, 1.0f, c->stream));
       RC(launch_resize_cubic_f32(mf + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 1, 1.0f, c->stream));
     }
+    side.leave();
   }
+  RC(side.join());
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
   // order and divided by the scale count: one pass per frame over the PAF and heat planes
   for (int f = 0; f < n; ++f) {

@@ -58,3 +58,25 @@ def test_library_resolves_its_own_symbols():
     out = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
     own = [l for l in out.splitlines() if "_ZN2op" in l or " op_" in l]
     assert not own, own
+
+
+@pytest.mark.parametrize("preset,keep,expect", [(None, None, "8"), ("4", None, "8"), ("16", None, "16"),
+                                                ("4", "1", "4")])
+def test_loader_hw_queue_default(preset, keep, expect):
+    """The loader gives detect_precise's side stream its own hardware queue: GPU_MAX_HW_QUEUES is
+    raised to 8 (a larger value kept; OP_KEEP_HW_QUEUES=1 keeps any value)."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    env.pop("OP_KEEP_HW_QUEUES", None)
+    if keep is not None:
+        env["OP_KEEP_HW_QUEUES"] = keep
+    if preset is not None:
+        env["GPU_MAX_HW_QUEUES"] = preset
+    code = ("import importlib, os, sys; sys.path.insert(0, %r); "
+            "m = importlib.import_module(%r + '._lib'); m.lib(); print(os.environ['GPU_MAX_HW_QUEUES'])"
+            % (REPO, PKG_NAME))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == expect
