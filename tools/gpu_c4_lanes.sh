@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the OP_PRECISE_LANES switch lived only in the experiment build; the second lane was not kept)
 # detect_precise: scale 1.5 on a second side stream (OP_PRECISE_LANES=2) vs one side stream (1):
 # precise parity tests with two lanes, then interleaved one-frame and 16-frame C4 lines.
 set -o pipefail
