@@ -74,7 +74,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libopenpose_hip.so is not built (%s); run __graft_entry__.build() or "
                            "make -C chainer_realtime_multi-person_pose_estimation_amd/csrc" % LIB_PATH)
-    # detect_precise runs its small scales on a side stream; with HIP's default 4 hardware queues per
+    # detect_precise can run its small scales on a side stream (OP_PRECISE_OVERLAP=1); with HIP's default 4 hardware queues per
     # process that stream shares a queue with the compute stream and nothing overlaps (one 1280x720
     # frame: 19.3 -> 15.5 ms at 8 queues).  Raised to 8 before the HIP runtime loads (a larger value
     # is kept; OP_KEEP_HW_QUEUES=1 keeps any value).

@@ -2376,7 +2376,9 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   // scales with <= 1/4 of the largest scale's network pixels (0.5 and 1.0 of the default 0.5/1/1.5/2)
   // run their forward + first map resize on the side stream, concurrently with the large scales:
   // same kernels and operands per scale, so the maps and the scale-ordered mean are unchanged
-  static const bool overlap = !(getenv("OP_PRECISE_OVERLAP") && atoi(getenv("OP_PRECISE_OVERLAP")) == 0);
+  // opt-in (OP_PRECISE_OVERLAP=1): one full GPU suite with the overlap live failed the 1280x720
+  // oracle test (max 8.0e-3 vs 2.0e-5; it passed in five other runs), cause not yet found
+  static const bool overlap = getenv("OP_PRECISE_OVERLAP") && atoi(getenv("OP_PRECISE_OVERLAP")) == 1;
   bool on_side[OP_MAX_SCALES] = {};
   {
     int64_t amax = 0;
