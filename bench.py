@@ -157,7 +157,8 @@ class Runner(object):
             p.array[...] = rng.integers(0, 256, (B, FH, FW, 3), dtype=np.uint8)
         self.k = 0
         self.persons = 0
-        self.over_caps = 0  # device-path frames whose record says "over the batched caps" (never re-run)
+        self.over_caps = 0  # device-path frames not delivered whole (must stay 0: overflow frames are re-run)
+        self.overflow = 0  # device-path frames delivered through the overflow message (re-run uncapped)
         # host path: the TCP fallback, detect_precise (full-resolution results), and workloads that
         # may exceed the batched post-process caps (fetch_results re-runs those frames uncapped)
         self.sync = not gather.device or bool(args.precise)
@@ -193,11 +194,13 @@ class Runner(object):
         self.k += 1
 
     def _collect(self):
-        raw = self.gather.g.wait(raw=True)
-        if self.pending.pop(0) and raw is not None:  # rank 0: every rank's records of that step
-            persons, over = self.Fr.count_persons(raw, GATHER_PERSONS)
+        got = self.gather.g.wait(raw=True)  # collective: also ships every rank's overflow frames
+        if self.pending.pop(0) and got is not None:  # rank 0: every rank's records of that step
+            raw, overflow = got
+            persons, missing = self.Fr.count_persons(raw, GATHER_PERSONS, overflow)
             self.persons += persons
-            self.over_caps += over
+            self.over_caps += missing
+            self.overflow += len(overflow)
 
     def drain(self):
         while self.pending:
@@ -386,7 +389,8 @@ def main():
                    "heatmap": "%dx%d" % optimal_size(FH, FW, 320) if not args.precise else "%dx%d" % (FW, FH),
                    "maps": args.maps, "parallelism": gather.label},
         "persons_per_s": round(persons / elapsed, 2),
-        "frames_over_caps": int(over_caps),  # device-record path: frames past the batched post-process caps
+        "frames_over_caps": int(over_caps),  # device-record path: frames not delivered whole (0 by design)
+        "frames_overflow": int(run.overflow),  # frames delivered whole through the overflow message
         "gflop_per_frame": round((sum(L.forward_flops(*precise_net(FH, FW, sc)) for sc in PARAMS_SCALES)
                                   if args.precise else L.forward_flops(net_h, net_w)) / 1e9, 2),
         "stage_ms_per_step": stage_ms,
@@ -397,22 +401,50 @@ def main():
         # side lines (not `value`): the same workload with the network's own maps, and in exact f32
         variants = {}
         vsteps = 5
+        # the random network's own maps, on the same asynchronous device-record path as the headline:
+        # frames past the batched post-process caps reach the host whole through the overflow
+        # re-runs (op_comm_overflow_result), timed on their own
         ctx.use_staged_maps(False)
-        run.sync = True  # the random network's maps can exceed the batched caps: fetch_results re-runs those
+        ov0, ovs0 = run.overflow, gather.g.overflow_s if gather.device else 0.0
         e, _ = measure(run, ctx, None, vsteps, 1, False)
-        run.sync = not gather.device or bool(args.precise)
-        variants["maps_network"] = {"value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
-                                    "note": "post-process on the random network's own last-stage maps"}
+        ovn = run.overflow - ov0
+        ovs = (gather.g.overflow_s - ovs0) if gather.device else 0.0
+        variants["maps_network"] = {
+            "value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
+            "path": "device records (async)" if not run.sync else "synchronous fetch",
+            "frames_overflow": ovn, "overflow_rerun_ms_per_step": round(ovs / (vsteps + 1) * 1e3, 3),
+            "note": "post-process on the random network's own last-stage maps (noise peaks); frames over the "
+                    "batched caps re-run alone uncapped on the host's collect path (counted over the warm-up "
+                    "and timed steps)"}
         if args.maps == "synthetic":
             ctx.use_staged_maps(True)
+        # exact f32 convolutions: the like-for-like arithmetic of the reference (Chainer fp32)
         ctx.set_precision("fp32")
         ctx.profile_classes(["conv7x7"])
         e, p32 = measure(run, ctx, None, vsteps, 1, True)
+        ctx.profile_classes(list(ctx.PROFILE_CLASSES))
+        ctx.profile(True)
+        ctx.profile_reset()
+        for _ in range(3):
+            run.step(False)
+        run.drain()
+        ctx.synchronize()
+        pall = ctx.profile_read()
+        ctx.profile(False)
         ms, n, fl, _ = p32["conv7x7"]
+        per_class = {}
+        for k in ("conv7x7", "conv3x3", "conv1x1"):
+            cms, cn, cfl, _ = pall[k]
+            if cn and cms > 0:
+                per_class[k] = {"ms_per_step": round(cms / 3, 3), "tflops": round(cfl / (cms * 1e-3) / 1e12, 2),
+                                "frac_of_157.3": round(cfl / (cms * 1e-3) / 1e12 / FP32_MATRIX_PEAK_TFLOPS, 4)}
         variants["fp32"] = {"value": round(B * vsteps / e, 2), "ms_per_step": round(e / vsteps * 1e3, 3),
                             "dtype": "f32 (exact f32 MFMA, v_mfma_f32_32x32x2_f32)",
                             "conv7x7_frac_of_157.3_TFLOPs": round(fl / (ms * 1e-3) / 1e12 / FP32_MATRIX_PEAK_TFLOPS, 4)
-                            if n else None}
+                            if n else None,
+                            "roofline_by_class": per_class,
+                            "stage_ms_per_step": {k: round(v[0] / 3, 3) for k, v in pall.items()},
+                            "stage_ms_note": "HIP-event sums per kernel class over 3 untimed profiled steps"}
         ctx.set_precision(args.precision)
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

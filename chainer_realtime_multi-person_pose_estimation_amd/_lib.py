@@ -25,9 +25,9 @@ EXPORTED = (
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_graph_info", "op_synchronize", "op_fetch_result",
     "op_last_timing", "op_forward_flops", "op_profile_enable", "op_profile_read", "op_profile_reset",
-    "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_host_alloc", "op_host_free",
+    "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_upload_wait", "op_conv_census", "op_host_alloc", "op_host_free",
     "op_pack_results", "op_comm_unique_id", "op_comm_create", "op_comm_destroy", "op_comm_gather_results",
-    "op_comm_wait", "op_detect_precise", "op_resize_cubic",
+    "op_comm_wait", "op_comm_overflow", "op_comm_overflow_result", "op_detect_precise", "op_resize_cubic",
     "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
@@ -74,17 +74,6 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libopenpose_hip.so is not built (%s); run __graft_entry__.build() or "
                            "make -C chainer_realtime_multi-person_pose_estimation_amd/csrc" % LIB_PATH)
-    # detect_precise can run its small scales on a side stream (OP_PRECISE_OVERLAP=1); with HIP's default 4 hardware queues per
-    # process that stream shares a queue with the compute stream and nothing overlaps (one 1280x720
-    # frame: 19.3 -> 15.5 ms at 8 queues).  Raised to 8 before the HIP runtime loads (a larger value
-    # is kept; OP_KEEP_HW_QUEUES=1 keeps any value).
-    if os.environ.get("OP_KEEP_HW_QUEUES") != "1":
-        try:
-            q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-        except ValueError:
-            q = 0
-        if q < 8:
-            os.environ["GPU_MAX_HW_QUEUES"] = "8"
     L = ctypes.CDLL(LIB_PATH)
     P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     sig = {
@@ -141,7 +130,11 @@ def lib():
         "op_comm_destroy": ([P], ctypes.c_int),
         "op_comm_gather_results": ([P, P, I32, I32, I32, ctypes.c_int64, I32], ctypes.c_int),
         "op_comm_wait": ([P, ctypes.c_double, P, P, P], ctypes.c_int),
+        "op_comm_overflow": ([P, P, P, I32, P], ctypes.c_int),
+        "op_comm_overflow_result": ([P, P, I32, P, P, I32, P], ctypes.c_int),
         "op_upload_frames": ([P, P, I32, I32, I32], ctypes.c_int),
+        "op_upload_wait": ([P], ctypes.c_int),
+        "op_conv_census": ([P, I32, I32], ctypes.c_int),
         "op_host_alloc": ([ctypes.c_size_t, P], ctypes.c_int),
         "op_host_free": ([P], ctypes.c_int),
         "op_fetch_maps": ([P, I32, I32, P, P, P, P], ctypes.c_int),
@@ -221,6 +214,21 @@ def layer_table():
     for i in range(N_LAYERS):
         check(lib().op_layer_info(i, ctypes.byref(name), ctypes.byref(ci), ctypes.byref(co), ctypes.byref(k)))
         out.append((name.value.decode(), ci.value, co.value, k.value))
+    return out
+
+
+CENSUS = {"7x7_splitk": 11, "7x7_other": 12, "3x3_w48": 13, "3x3_w32": 14, "3x3_pool": 15, "3x3_splitk": 16,
+          "3x3_big": 17, "conv1_pair": 18}
+CENSUS_SLOTS = 24
+
+
+def conv_census(reset=False):
+    """Process-wide launch counts of the bf16x3 conv kernels (op_conv_census): {"npx": {NPX: n}
+    for the 7x7 raster kernel, plus the CENSUS slots by name}."""
+    a = (ctypes.c_int32 * CENSUS_SLOTS)()
+    check(lib().op_conv_census(a, CENSUS_SLOTS, 1 if reset else 0), "op_conv_census")
+    out = {"npx": {i: a[i] for i in range(1, 11) if a[i]}}
+    out.update({k: a[v] for k, v in CENSUS.items()})
     return out
 
 
@@ -449,11 +457,16 @@ class Context(object):
 
     def upload_frames(self, frames):
         """Asynchronous staging (op_upload_frames): the next run_staged* uses these frames; keep
-        `frames` (ideally a PinnedFrames array) unchanged until that run is enqueued."""
+        `frames` (ideally a PinnedFrames array) unchanged until the copy has completed
+        (upload_wait(), synchronize(), or a later call that waited for the consuming run)."""
         if frames.dtype != np.uint8 or frames.ndim != 4 or frames.shape[3] != 3 or not frames.flags.c_contiguous:
             raise ValueError("expected contiguous (n, h, w, 3) uint8 frames")
         n, h, w, _ = frames.shape
         check(lib().op_upload_frames(self.h, ctypes.c_void_p(frames.ctypes.data), n, h, w), "op_upload_frames")
+
+    def upload_wait(self):
+        """Block until every upload_frames copy has finished reading its host buffer."""
+        check(lib().op_upload_wait(self.h), "op_upload_wait")
 
     def stage_maps(self, maps):
         maps = np.ascontiguousarray(maps, dtype=np.float32)

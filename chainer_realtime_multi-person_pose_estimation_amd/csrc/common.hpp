@@ -123,6 +123,9 @@ int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream
 // big-tile 7x7 kernel (conv_big.hip): one workgroup per CU, 128 channels x <= 768 pixels
 int conv_big_device_init(int device);  // per-device constants; call once per context, outside capture
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
+// process-wide launch census of the bf16x3 conv kernels by instantiation (op_conv_census; slots in
+// include/openpose_hip.h): incremented on the host at every launch (a graph replay adds nothing)
+void census_add(int slot);
 // 3x3 conv + ReLU + 2x2 max-pool fused (conv_big.hip)
 int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
 // fused 1x1 pair at the end of a branch (conv_head.hip): in -> W1 (ReLU) -> W2 (no ReLU) -> out

@@ -265,6 +265,7 @@ int launch_conv1_pair(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
     attr = true;
   }
   const dim3 grid((unsigned)((w + kP1C - 1) / kP1C), (unsigned)((h + kP1R - 1) / kP1R), (unsigned)n);
+  census_add(OP_CENSUS_CONV1_PAIR);
   if (frames)
     hipLaunchKernelGGL(conv1_pair_bf16x3<true>, grid, dim3(256), lds, st, frames, frame_bytes, row_stride, sh, sw,
                        nullptr, h, w, wt11, b11, (const char*)w12, b12, (char*)out, pout);

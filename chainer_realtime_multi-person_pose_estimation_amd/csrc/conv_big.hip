@@ -20,6 +20,7 @@
 //  * Workgroup -> XCD: blocks are dealt to XCDs round-robin, so block b is remapped to make every
 //    XCD work on ONE weight set (branch x channel tile), which its 4 MiB L2 then holds.
 //  * MFMA: v_mfma_f32_32x32x16_bf16, products hi*hi + hi*lo + lo*hi into one f32 accumulator.
+#include <atomic>
 #include <array>
 #include <map>
 #include <mutex>
@@ -395,6 +396,11 @@ int conv_big_device_init(int device) {
   return OP_OK;
 }
 
+static std::atomic<int64_t> g_census[OP_CENSUS_SLOTS];
+void census_add(int slot) {
+  if (slot >= 0 && slot < OP_CENSUS_SLOTS) g_census[slot].fetch_add(1, std::memory_order_relaxed);
+}
+
 static const void* device_zeros() {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) return nullptr;
@@ -584,6 +590,7 @@ static int launch_big_t(const SplitConvShape& s, const SplitConvGroup* g, const 
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
+  census_add(KS == 7 ? OP_CENSUS_7X7_OTHER : OP_CENSUS_3X3_BIG);
   hipLaunchKernelGGL((conv_big_bf16x3<KS, NPB, NWAVE, CW, PAIR, POOL, RASTER>), dim3(blocks), dim3(NWAVE * 64), lds, st, s, g[0],
                      s.groups > 1 ? g[1] : g[0], tl);
   OP_AFTER_LAUNCH("conv_big_bf16x3", st);
@@ -723,6 +730,8 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
     }
   }
   const dim3 grid(blocks, (unsigned)t.ksplit);
+  census_add(pool ? OP_CENSUS_3X3_POOL : tl.tc == 48 ? OP_CENSUS_3X3_W48 : OP_CENSUS_3X3_W32);
+  if (t.ksplit > 1) census_add(OP_CENSUS_3X3_SPLITK);
   if (pool)
     hipLaunchKernelGGL(conv_m16k_bf16x3<true>, grid, dim3(256), lds, st, s, g[0], g1, t);
   else if (tl.tc == 48) {
@@ -868,6 +877,8 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         }
       }
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+      census_add(npx);
+      if (tl.ksplit > 1) census_add(OP_CENSUS_7X7_SPLITK);
       const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
       if (rc != OP_OK) return rc;
       if (tl.ksplit > 1) {
@@ -908,3 +919,13 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
 }
 
 }  // namespace op
+
+int op_conv_census(int32_t* counts, int32_t n, int32_t reset) {
+  if (!counts || n < 1) return OP_ERR_INVALID;
+  for (int i = 0; i < OP_CENSUS_SLOTS; ++i) {
+    const int64_t v = reset ? op::g_census[i].exchange(0) : op::g_census[i].load();
+    if (i < n) counts[i] = (int32_t)std::min<int64_t>(v, INT32_MAX);
+  }
+  for (int i = OP_CENSUS_SLOTS; i < n; ++i) counts[i] = 0;
+  return OP_OK;
+}

@@ -23,7 +23,10 @@
 
 extern "C" int64_t record_bytes(int max_persons);
 extern "C" int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame_base, int frame_stride,
-                                void* dst, hipStream_t* stream);
+                                void* dst, hipStream_t* stream, int keep_slot);
+extern "C" int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t cap, int32_t* count);
+extern "C" int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* scores, int32_t cap,
+                               op_frame_result* res);
 extern "C" int ctx_device(op_ctx* c);
 
 struct op_comm {
@@ -38,6 +41,7 @@ struct op_comm {
   int next = 0;                         // slot of the next submit
   int queued[2] = {0, 0};               // frames (all ranks) of an outstanding gather per slot, 0 = none
   int64_t rbytes[2] = {0, 0};
+  int last = -1;                        // slot op_comm_wait returned last (op_comm_overflow*)
   int order[2] = {-1, -1};              // FIFO of outstanding slots
   bool aborted = false;
   double timeout_s = 0.0;               // op_comm_create's per-rank timeout (init and enqueue waits)
@@ -218,7 +222,7 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
     if (g->rank == 0) g->all_cap = std::max(g->all_cap, all);
   }
   hipStream_t cst;
-  RC(ctx_pack_records(ctx, first, n, max_persons, frame_base, frame_stride, g->d_rec[k], &cst));
+  RC(ctx_pack_records(ctx, first, n, max_persons, frame_base, frame_stride, g->d_rec[k], &cst, k));
   OP_HIP_CHECK(hipEventRecord(g->ev_packed[k], cst));
   OP_HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_packed[k], 0));
   ncclResult_t r = ncclGather(g->d_rec[k], g->rank == 0 ? g->d_all[k] : nullptr, mine, ncclUint8, 0, g->comm, g->stream);
@@ -265,10 +269,37 @@ int op_comm_wait(op_comm* g, double timeout_s, const void** records, int32_t* n_
   const int nf = g->queued[k];
   g->queued[k] = 0;
   if (rc) return rc;
+  g->last = k;
   *records = g->rank == 0 ? g->h_all[k] : nullptr;
   *n_frames = g->rank == 0 ? nf : 0;
   *rec_bytes = g->rbytes[k];
   return OP_OK;
+}
+
+int op_comm_overflow(op_comm* g, op_ctx* ctx, int32_t* frames, int32_t cap, int32_t* count) {
+  if (!g || !ctx || !count) {
+    set_error("op_comm_overflow: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  if (g->last < 0) {
+    set_error("op_comm_overflow: no gather waited for yet");
+    return OP_ERR_STATE;
+  }
+  return ctx_kept_overflow(ctx, g->last, frames, cap, count);
+}
+
+int op_comm_overflow_result(op_comm* g, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,
+                            op_frame_result* res) {
+  if (!g || !ctx) {
+    set_error("op_comm_overflow_result: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  if (g->last < 0) {
+    set_error("op_comm_overflow_result: no gather waited for yet");
+    return OP_ERR_STATE;
+  }
+  OP_HIP_CHECK(hipSetDevice(g->device));
+  return ctx_kept_result(ctx, g->last, frame, poses, scores, cap, res);
 }
 
 }  // extern "C"

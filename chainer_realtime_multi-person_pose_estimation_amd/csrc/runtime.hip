@@ -225,6 +225,22 @@ struct PostRecord {
   PostShape s{};
 };
 
+// Per gather slot (gather.hip's two record slots): the post-process input of the frames whose
+// record cannot carry the whole result (over the batched caps, or more persons than the record
+// holds), copied aside on the device when the records are packed, so the owning rank can re-run
+// them after the next step has overwritten the batched buffers (op_comm_overflow*).
+struct KeepSlot {
+  float* maps = nullptr;
+  size_t maps_cap = 0;  // bytes
+  int32_t* cnt = nullptr;
+  size_t cnt_cap = 0;
+  int32_t* d_hdr = nullptr;  // n x {status, n_peaks, n_persons, flagged}
+  int32_t* h_hdr = nullptr;  // pinned copy, complete when the slot's gather is
+  size_t hdr_cap = 0;
+  PostRecord rec{};
+  int n = 0;
+};
+
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
   B_S1, B_MAP32, B_COUNT
@@ -280,10 +296,6 @@ struct op_ctx {
   // async frame uploads (op_upload_frames): a 2-slot device ring filled on copy_stream; the next
   // run waits for its slot's copy and moves it into d_frames on the compute stream
   hipStream_t copy_stream = nullptr;
-  // detect_precise: the scales with at most a quarter of the largest scale's network pixels run on
-  // this side stream, concurrently with the large ones (their launches fill a fraction of the chip)
-  hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* d_ring[2] = {nullptr, nullptr};
   size_t ring_bytes[2] = {0, 0};
   hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -328,9 +340,15 @@ struct op_ctx {
   // pinned host staging for batched result fetches
   char* host_stage = nullptr;
   size_t host_stage_bytes = 0;
+  // pinned host staging for the one-frame uploads of op_detect / op_detect_precise: the caller's
+  // (pageable, possibly row-strided) image is packed here by the host and copied with one plain
+  // async copy on the compute stream -- no pageable or 2D copy path of the HIP runtime is involved
+  uint8_t* up_pinned = nullptr;
+  size_t up_pinned_bytes = 0;
   // uncapped post-process: the last batched post-process's input (to re-run one frame) and the
   // one-frame big-mode buffers sized from that frame's own counts
   op::PostRecord post_rec;
+  op::KeepSlot keep[2];
   PostBuffers bigb{};
   void* bb_arena = nullptr;
   int big_frame = -1;  // frame of post_rec whose big-mode result sits in bb
@@ -389,8 +407,10 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
       size_t lru = 0;
       for (size_t i = 1; i < c->arenas.size(); ++i)
         if (c->arenas[i].used < c->arenas[lru].used) lru = i;
+      // every stream that may still read the arena: the compute stream and the upload ring's copy
+      // stream (which touches only d_ring, but hipFree must not race any queued work)
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
-      if (c->side_stream) OP_HIP_CHECK(hipStreamSynchronize(c->side_stream));  // the other stream's arenas
+      if (c->copy_stream) OP_HIP_CHECK(hipStreamSynchronize(c->copy_stream));
       guard_forget(c->arenas[lru].p, c->arenas[lru].bytes);
       OP_HIP_CHECK(hipFree(c->arenas[lru].p));
       c->arenas.erase(c->arenas.begin() + lru);
@@ -972,24 +992,21 @@ static int post_one_frame(op_ctx* c, const PostRecord& r, int f, PostBuffers& B)
   return launch_grouping(s1, B, c->stream);
 }
 
-// Re-run frame f of the last batched post-process in big mode; *out = buffers holding its result.
-static int rerun_big(op_ctx* c, int f, PostBuffers** out) {
-  if (c->big_frame == f && c->bb_arena) {
-    *out = &c->bigb;
-    return OP_OK;
-  }
-  const PostRecord r = c->post_rec;
+// Re-run frame f of the recorded post-process input r in big mode, sizing the buffers from the
+// frame's batched peak counts at d_cnt (18 int32); *out = buffers holding its result.
+static int rerun_big_rec(op_ctx* c, const PostRecord& r, int f, const int32_t* d_cnt, PostBuffers** out) {
   if (r.kind == 0 || f < 0 || f >= r.s.n) {
     set_error("post-process capacity exceeded and no recorded input to re-run the frame");
     return OP_ERR_CAPACITY;
   }
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   int32_t cnt[OP_N_JOINTS];
-  OP_HIP_CHECK(hipMemcpy(cnt, c->pb.peak_cnt + (size_t)f * OP_N_JOINTS, sizeof(cnt), hipMemcpyDeviceToHost));
+  OP_HIP_CHECK(hipMemcpy(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
   int maxp = 1;
   for (int j = 0; j < OP_N_JOINTS; ++j) maxp = std::max(maxp, cnt[j]);
   int64_t maxc = std::min<int64_t>((int64_t)maxp * maxp, (int64_t)1 << 20);
   PostBuffers* B = nullptr;
+  c->big_frame = -1;
   for (;;) {
     RC(big_buffers(c, maxp, maxc, &B));
     RC(post_one_frame(c, r, f, *B));
@@ -1001,8 +1018,45 @@ static int rerun_big(op_ctx* c, int f, PostBuffers** out) {
     if (need <= B->maxc) break;
     maxc = need;  // more candidates than the first guess: grow and run again
   }
-  c->big_frame = f;
   *out = B;
+  return OP_OK;
+}
+
+// Re-run frame f of the last batched post-process in big mode (cached per frame).
+static int rerun_big(op_ctx* c, int f, PostBuffers** out) {
+  if (c->big_frame == f && c->bb_arena) {
+    *out = &c->bigb;
+    return OP_OK;
+  }
+  if (c->post_rec.kind == 0 || f < 0 || f >= c->post_rec.s.n) {
+    set_error("post-process capacity exceeded and no recorded input to re-run the frame");
+    return OP_ERR_CAPACITY;
+  }
+  RC(rerun_big_rec(c, c->post_rec, f, c->pb.peak_cnt + (size_t)f * OP_N_JOINTS, out));
+  c->big_frame = f;
+  return OP_OK;
+}
+
+// The result of a one-frame big-mode buffer set (frame 0 of B) into the caller's arrays.
+static int read_big(PostBuffers* B, double* poses, double* scores, int cap, op_frame_result* res) {
+  int32_t hdr[4];
+  OP_HIP_CHECK(hipMemcpy(hdr, B->res_hdr, sizeof(hdr), hipMemcpyDeviceToHost));
+  res->status = hdr[0];
+  res->n_peaks = hdr[1];
+  res->n_persons = hdr[0] == OP_OK ? hdr[2] : 0;
+  if (hdr[0] != OP_OK) {
+    set_error(hdr[0] == OP_ERR_INDEX ? "list assignment index out of range (grouping_key_points)"
+                                     : "post-process capacity exceeded (peaks per joint / subsets)");
+    return hdr[0];
+  }
+  if (hdr[2] > cap) {
+    set_error("result capacity too small");
+    return OP_ERR_CAPACITY;
+  }
+  if (hdr[2] > 0) {
+    OP_HIP_CHECK(hipMemcpy(poses, B->res_poses, (size_t)hdr[2] * 54 * 8, hipMemcpyDeviceToHost));
+    OP_HIP_CHECK(hipMemcpy(scores, B->res_scores, (size_t)hdr[2] * 8, hipMemcpyDeviceToHost));
+  }
   return OP_OK;
 }
 
@@ -1220,7 +1274,7 @@ int op_destroy(op_ctx* c) {
   if (!c) return OP_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  if (c->side_stream) hipStreamSynchronize(c->side_stream);
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
   free_weights(c);
@@ -1245,6 +1299,13 @@ int op_destroy(op_ctx* c) {
   if (c->d_pmid) hipFree(c->d_pmid);
   if (c->d_psum) hipFree(c->d_psum);
   if (c->host_stage) hipHostFree(c->host_stage);
+  if (c->up_pinned) hipHostFree(c->up_pinned);
+  for (auto& k : c->keep) {
+    if (k.maps) hipFree(k.maps);
+    if (k.cnt) hipFree(k.cnt);
+    if (k.d_hdr) hipFree(k.d_hdr);
+    if (k.h_hdr) hipHostFree(k.h_hdr);
+  }
   if (c->bb_arena) hipFree(c->bb_arena);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -1253,13 +1314,6 @@ int op_destroy(op_ctx* c) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
   }
-  if (c->side_stream) {
-    (void)hipStreamSynchronize(c->side_stream);
-    splitk_ws_release(c->side_stream);
-    (void)hipStreamDestroy(c->side_stream);
-  }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (int i = 0; i < 2; ++i) {
     if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
     if (c->ev_up[i]) (void)hipEventDestroy(c->ev_up[i]);
@@ -1704,6 +1758,9 @@ static int stage_maps_dev(op_ctx* c, const float* maps, int n, int lh, int lw, f
         for (int x = 0; x < lw; ++x)
           t[(((size_t)f * lh + y) * lw + x) * 57 + ch] = maps[(((size_t)f * 57 + ch) * lh + y) * lw + x];
   RC(grow_buffer(c, (void**)&c->d_maps, &c->maps_bytes, fl * 4, "maps"));
+  // the null-stream copy is not ordered against the (non-blocking) compute stream: a queued run may
+  // still read the old maps
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   OP_HIP_CHECK(hipMemcpy(c->d_maps, t.data(), fl * 4, hipMemcpyHostToDevice));
   *out = c->d_maps;
   return OP_OK;
@@ -1819,6 +1876,7 @@ int op_stage_maps(op_ctx* c, const float* maps, int32_t n, int32_t mh, int32_t m
     const size_t bytes = (size_t)n * 57 * mh * mw * 4;
     c->post_rec.kind = 0;  // staged maps are replaced
     RC(grow_buffer(c, (void**)&c->d_fmaps, &c->fmaps_bytes, bytes, "full_maps"));
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));  // a queued precise run may still read the old maps
     OP_HIP_CHECK(hipMemcpy(c->d_fmaps, maps, bytes, hipMemcpyHostToDevice));
     c->fm_n = n;
     c->fm_h = mh;
@@ -1905,6 +1963,14 @@ int op_upload_frames(op_ctx* c, const uint8_t* frames, int32_t n, int32_t h, int
   c->up_h = h;
   c->up_w = w;
   c->ring_next = k ^ 1;
+  return OP_OK;
+}
+
+int op_upload_wait(op_ctx* c) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  for (int k = 0; k < 2; ++k)
+    if (c->ev_up[k]) OP_HIP_CHECK(hipEventSynchronize(c->ev_up[k]));
   return OP_OK;
 }
 
@@ -2174,19 +2240,115 @@ __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, in
 
 int64_t record_bytes(int max_persons) { return 32 + (int64_t)max_persons * 55 * 8; }
 
-// Enqueue the records of staged frames [first, first+n) into dst (device) on the context stream.
+// Keep slot fill (see KeepSlot): per frame, its header and whether the record cannot carry the
+// whole result; for those frames, the recorded post-process input and batched peak counts.
+__global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, int max_persons, const float* __restrict__ src,
+                                                     int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
+                                                     int32_t* __restrict__ hdr) {
+  const int i = blockIdx.x;
+  const int f = first + i;
+  const int status = b.res_hdr[4 * f];
+  const int persons = b.res_hdr[4 * f + 2];
+  const int flag = status == OP_ERR_CAPACITY || (status == OP_OK && persons > max_persons);
+  if (threadIdx.x == 0) {
+    hdr[4 * i] = status;
+    hdr[4 * i + 1] = b.res_hdr[4 * f + 1];
+    hdr[4 * i + 2] = status == OP_OK ? persons : 0;
+    hdr[4 * i + 3] = flag;
+  }
+  if (!flag || !src) return;
+  if (threadIdx.x < OP_N_JOINTS) cnt[i * OP_N_JOINTS + threadIdx.x] = b.peak_cnt[f * OP_N_JOINTS + threadIdx.x];
+  const float* s = src + (int64_t)f * fstride;
+  float* d = dst + (int64_t)i * fstride;
+  for (int64_t e = threadIdx.x; e < fstride; e += 256) d[e] = s[e];
+}
+
+// Enqueue the records of staged frames [first, first+n) into dst (device) on the context stream;
+// keep_slot 0/1 also fills that keep slot (gather.hip passes its record slot) and copies its
+// headers to pinned memory on the same stream.
 int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame_base, int frame_stride, void* dst,
-                     hipStream_t* stream) {
-  if (first < 0 || n < 1 || first + n > c->st_n || first + n > c->pn || max_persons < 0) {
+                     hipStream_t* stream, int keep_slot) {
+  if (first < 0 || n < 1 || first + n > c->st_n || first + n > c->pn || max_persons < 0 || keep_slot > 1) {
     set_error("pack records: bad frame range");
     return OP_ERR_INVALID;
   }
   hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
                      frame_stride, (char*)dst, record_bytes(max_persons));
   OP_AFTER_LAUNCH("pack_records", c->stream);
+  if (keep_slot >= 0) {
+    KeepSlot& k = c->keep[keep_slot];
+    const PostRecord& r = c->post_rec;
+    const float* src = r.kind == 1 ? r.low.base : r.kind == 2 ? r.full : nullptr;
+    const int64_t fstride = r.kind == 1 ? r.low.fstride : r.fstride;
+    if (src) {
+      RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)n * fstride * 4, "keep_maps"));
+      RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)n * OP_N_JOINTS * 4, "keep_cnt"));
+    }
+    const size_t hb = (size_t)n * 16;
+    if (hb > k.hdr_cap) {
+      OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      if (k.d_hdr) OP_HIP_CHECK(hipFree(k.d_hdr));
+      if (k.h_hdr) OP_HIP_CHECK(hipHostFree(k.h_hdr));
+      k.d_hdr = nullptr;
+      k.h_hdr = nullptr;
+      k.hdr_cap = 0;
+      OP_HIP_CHECK(hipMalloc((void**)&k.d_hdr, hb));
+      OP_HIP_CHECK(hipHostMalloc((void**)&k.h_hdr, hb, hipHostMallocDefault));
+      k.hdr_cap = hb;
+    }
+    hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
+                       k.maps, k.cnt, k.d_hdr);
+    OP_AFTER_LAUNCH("keep_overflow", c->stream);
+    OP_HIP_CHECK(hipMemcpyAsync(k.h_hdr, k.d_hdr, hb, hipMemcpyDeviceToHost, c->stream));
+    k.rec = r;
+    k.rec.s.n = n;
+    if (r.kind == 1) k.rec.low.base = k.maps;
+    else if (r.kind == 2) k.rec.full = k.maps;
+    if (!src) k.rec.kind = 0;
+    k.n = n;
+  }
   OP_HIP_CHECK(hipGetLastError());
   *stream = c->stream;
   return OP_OK;
+}
+
+// This rank's frames (slot-relative) of keep slot `slot` whose record does not carry the whole
+// result; valid once the slot's gather has completed (op_comm_wait).
+int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t cap, int32_t* count) {
+  if (slot < 0 || slot > 1 || !count || (cap > 0 && !frames)) {
+    set_error("kept overflow: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  const KeepSlot& k = c->keep[slot];
+  int m = 0;
+  for (int i = 0; i < k.n; ++i)
+    if (k.h_hdr[4 * i + 3]) {
+      if (m < cap) frames[m] = i;
+      ++m;
+    }
+  *count = m;
+  return OP_OK;
+}
+
+// Full result of frame i of keep slot `slot` (re-run alone in big mode from the kept input).
+int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* scores, int32_t cap, op_frame_result* res) {
+  if (slot < 0 || slot > 1 || !res || !poses || !scores || frame < 0 || frame >= c->keep[slot].n) {
+    set_error("kept result: bad arguments");
+    return OP_ERR_INVALID;
+  }
+  KeepSlot& k = c->keep[slot];
+  memset(res, 0, sizeof(*res));
+  if (!k.h_hdr[4 * frame + 3]) {
+    set_error("kept result: the frame's record carries its whole result");
+    return OP_ERR_STATE;
+  }
+  if (k.rec.kind == 0) {
+    set_error("kept result: no recorded post-process input for this slot");
+    return OP_ERR_STATE;
+  }
+  PostBuffers* B = nullptr;
+  RC(rerun_big_rec(c, k.rec, frame, k.cnt + (size_t)frame * OP_N_JOINTS, &B));
+  return read_big(B, poses, scores, cap, res);
 }
 
 int ctx_device(op_ctx* c) { return c->device; }
@@ -2202,7 +2364,7 @@ int op_pack_results(op_ctx* c, int32_t first, int32_t n, int32_t max_persons, in
   const size_t bytes = (size_t)n * record_bytes(max_persons);
   RC(ensure_scratch(c, bytes));
   hipStream_t st;
-  RC(ctx_pack_records(c, first, n, max_persons, frame_base, frame_stride, c->d_scratch, &st));
+  RC(ctx_pack_records(c, first, n, max_persons, frame_base, frame_stride, c->d_scratch, &st, -1));
   OP_HIP_CHECK(hipMemcpyAsync(host_records, c->d_scratch, bytes, hipMemcpyDeviceToHost, st));
   OP_HIP_CHECK(hipStreamSynchronize(st));
   return OP_OK;
@@ -2278,6 +2440,24 @@ int op_fetch_results(op_ctx* c, int32_t first, int32_t n, double* poses, double*
   return OP_OK;
 }
 
+// One frame (h x w x 3 u8, row stride row_stride) from caller memory into d_frames on the compute
+// stream, through the context's page-locked staging buffer (op_detect / op_detect_precise).
+static int upload_one_frame(op_ctx* c, const uint8_t* bgr, int h, int w, int64_t row_stride) {
+  const size_t row = (size_t)w * 3, bytes = row * h;
+  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));  // the staging buffer's previous copy has completed
+  if (bytes > c->up_pinned_bytes) {
+    if (c->up_pinned) OP_HIP_CHECK(hipHostFree(c->up_pinned));
+    c->up_pinned = nullptr;
+    c->up_pinned_bytes = 0;
+    OP_HIP_CHECK(hipHostMalloc((void**)&c->up_pinned, bytes, hipHostMallocDefault));
+    c->up_pinned_bytes = bytes;
+  }
+  for (int y = 0; y < h; ++y) memcpy(c->up_pinned + (size_t)y * row, bgr + (size_t)y * row_stride, row);
+  OP_HIP_CHECK(hipMemcpyAsync(c->d_frames, c->up_pinned, bytes, hipMemcpyHostToDevice, c->stream));
+  return OP_OK;
+}
+
 int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_stride, double* poses, double* scores,
               int32_t cap, op_frame_result* res) {
   using namespace op;
@@ -2286,11 +2466,8 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
     set_error("op_detect: bad arguments");
     return OP_ERR_INVALID;
   }
-  const size_t bytes = (size_t)h * w * 3;
   c->up_slot = -1;  // a pending op_upload_frames is replaced
-  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
-  OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
-                                hipMemcpyHostToDevice, c->stream));
+  RC(upload_one_frame(c, bgr, h, w, row_stride));
   c->st_n = 1;
   c->st_h = h;
   c->st_w = w;
@@ -2303,48 +2480,6 @@ int op_detect(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64_t row_s
   RC(guard_check("op_detect"));
   return op_fetch_result(c, 0, poses, scores, cap, res);
 }
-
-// Runs a part of the enqueue on c->side_stream: enter() points c->stream at the side stream (the
-// first time, after a fork event on the compute stream, so it sees everything enqueued so far),
-// leave() points it back; join() -- also run on scope exit, so an error return leaves no side work
-// unjoined -- makes the compute stream wait for the side stream's work.
-struct SideStream {
-  op_ctx* c;
-  hipStream_t main;
-  bool forked = false, inside = false;
-  explicit SideStream(op_ctx* ctx) : c(ctx), main(ctx->stream) {}
-  int enter() {
-    if (!c->side_stream) {
-      // its own hardware queue only when the process has more than HIP's default 4 (the compute,
-      // copy and communicator streams and the null stream take those): the Python loader raises
-      // GPU_MAX_HW_QUEUES to 8
-      OP_HIP_CHECK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    }
-    if (!forked) {
-      OP_HIP_CHECK(hipEventRecord(c->ev_fork, main));
-      OP_HIP_CHECK(hipStreamWaitEvent(c->side_stream, c->ev_fork, 0));
-      forked = true;
-    }
-    c->stream = c->side_stream;
-    inside = true;
-    return OP_OK;
-  }
-  void leave() {
-    c->stream = main;
-    inside = false;
-  }
-  int join() {
-    leave();
-    if (!forked) return OP_OK;
-    forked = false;
-    OP_HIP_CHECK(hipEventRecord(c->ev_join, c->side_stream));
-    OP_HIP_CHECK(hipStreamWaitEvent(main, c->ev_join, 0));
-    return OP_OK;
-  }
-  ~SideStream() { (void)join(); }
-};
 
 // detect_precise (pose_detector.py:433-482).  Sizes follow the reference's Python arithmetic:
 // multiplier = scale * inference_img_size / min(h, w) and math.ceil(w * multiplier) in f64.
@@ -2373,22 +2508,8 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_off[ns] * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;
-  // scales with <= 1/4 of the largest scale's network pixels (0.5 and 1.0 of the default 0.5/1/1.5/2)
-  // run their forward + first map resize on the side stream, concurrently with the large scales:
-  // same kernels and operands per scale, so the maps and the scale-ordered mean are unchanged
-  // opt-in (OP_PRECISE_OVERLAP=1): one full GPU suite with the overlap live failed the 1280x720
-  // oracle test (max 8.0e-3 vs 2.0e-5; it passed in five other runs), cause not yet found
-  static const bool overlap = getenv("OP_PRECISE_OVERLAP") && atoi(getenv("OP_PRECISE_OVERLAP")) == 1;
-  bool on_side[OP_MAX_SCALES] = {};
-  {
-    int64_t amax = 0;
-    for (int k = 0; k < ns; ++k) amax = std::max(amax, (int64_t)phs[k] * pws[k]);
-    for (int k = 0; k < ns; ++k) on_side[k] = overlap && ns > 1 && (int64_t)phs[k] * pws[k] * 4 <= amax;
-  }
-  SideStream side(c);
   for (int k = 0; k < ns; ++k) {
     const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
-    if (on_side[k]) RC(side.enter());
     RC(ensure_geometry(c, n, ph, pw));
     const Act& x0 = c->buf[B_X0];
     for (int f = 0; f < n; ++f)
@@ -2428,9 +2549,7 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       RC(launch_resize_cubic_f32(mf + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 1, 1.0f, c->stream));
       RC(launch_resize_cubic_f32(mf + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 1, 1.0f, c->stream));
     }
-    side.leave();
   }
-  RC(side.join());
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
   // order and divided by the scale count: one pass per frame over the PAF and heat planes
   for (int f = 0; f < n; ++f) {
@@ -2480,11 +2599,8 @@ int op_detect_precise(op_ctx* c, const uint8_t* bgr, int32_t h, int32_t w, int64
     set_error("op_detect_precise: bad arguments (frame >= 11 x 11, at least one inference scale)");
     return OP_ERR_INVALID;
   }
-  const size_t bytes = (size_t)h * w * 3;
   c->up_slot = -1;  // a pending op_upload_frames is replaced
-  RC(grow_buffer(c, (void**)&c->d_frames, &c->frames_bytes, bytes, "frames"));
-  OP_HIP_CHECK(hipMemcpy2DAsync(c->d_frames, (size_t)w * 3, bgr, (size_t)row_stride, (size_t)w * 3, h,
-                                hipMemcpyHostToDevice, c->stream));
+  RC(upload_one_frame(c, bgr, h, w, row_stride));
   // the staged frame set is replaced by this frame (its result stays fetchable as frame 0)
   c->st_n = 0;
   int net_w = 0, net_h = 0;

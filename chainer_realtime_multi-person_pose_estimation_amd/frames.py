@@ -11,6 +11,12 @@ result records to rank 0 (include/openpose_hip.h "Multi-GPU result gather"):
 * ``HostGather`` -- the same records and control flow over TCP sockets from host memory (CPU
   tests, world size 2, and any rank without a GPU).
 
+Every frame reaches rank 0 whole, like the reference's ``__call__`` returns every frame's poses: a
+record carries at most ``max_persons`` persons and no persons for a frame over the batched
+post-process caps, so each rank also ships the whole results of its own such frames ("overflow",
+re-run on its device from the post-process input the library kept aside, op_comm_overflow*) over
+the TCP transport, and rank 0 merges them into the gathered records.
+
 ``SocketTransport`` is the small TCP star (rank 0 = hub) both use for bootstrap (RCCL's unique id),
 barriers and scalar max-reductions; every receive has a timeout, so a stalled rank fails loudly
 (``TimeoutError``) instead of hanging the job (SURVEY §5 failure detection).
@@ -70,14 +76,46 @@ def unpack_records(buf, max_persons):
     return out
 
 
-def count_persons(buf, max_persons):
-    """(sum of the exact per-frame person counts, frames whose status is OP_ERR_CAPACITY = over
-    the batched post-process caps, to be fetched with op_fetch_result) of packed records."""
+def pack_full(results):
+    """Whole results of any person count (the overflow message): int32 n, int32 persons per record,
+    then pack_records of them at that size."""
+    mp = max([len(r[4]) for r in results if r[1] == 0] + [0])
+    return struct.pack("<ii", len(results), mp) + pack_records(results, mp).tobytes()
+
+
+def unpack_full(buf):
+    n, mp = struct.unpack("<ii", bytes(buf[:8]))
+    return unpack_records(bytes(buf[8:]), mp) if n else []
+
+
+def merge_overflow(records, overflow):
+    """Records (unpacked) with the whole results of the overflow frames in place of theirs."""
+    if not overflow:
+        return records
+    by_id = {r[0]: r for r in overflow}
+    return [by_id.get(r[0], r) for r in records]
+
+
+def count_persons(buf, max_persons, overflow=()):
+    """(persons of every frame, frames still not delivered whole) of packed records plus the
+    overflow results of the frames they could not carry.  Header person counts are exact even
+    past max_persons; a frame over the batched caps counts its overflow result's persons (and
+    counts as undelivered only when no overflow result came for it)."""
     rb = record_bytes(max_persons)
     a = np.frombuffer(buf, np.uint8).reshape(-1, rb)
-    hdr = np.ascontiguousarray(a[:, :HDR_BYTES]).view(np.int32)  # status, n_peaks, n_persons, ...
-    ok = hdr[:, 0] == 0
-    return int(hdr[ok, 2].sum()), int((hdr[:, 0] == STATUS_CAPACITY).sum())
+    hdr = np.ascontiguousarray(a[:, :HDR_BYTES]).view(np.int32)  # status, n_peaks, n_persons, 0, id lo/hi
+    fid = np.ascontiguousarray(a[:, 16:24]).view(np.int64).reshape(-1)
+    ovf = {r[0]: r for r in overflow}
+    persons, missing = 0, 0
+    for i in range(len(a)):
+        r = ovf.get(int(fid[i]))
+        if r is not None:
+            persons += len(r[4]) if r[1] == 0 else 0
+        elif hdr[i, 0] == 0:
+            persons += int(hdr[i, 2])
+        elif hdr[i, 0] == STATUS_CAPACITY:
+            missing += 1
+    return persons, missing
 
 
 # ---------------------------------------------------------------- transport
@@ -211,15 +249,23 @@ class HostGather(object):
         self.pending = []
 
     def submit(self, results):
-        """results: this rank's [(frame_id, status, n_peaks, poses, scores)] of one step."""
-        self.pending.append(pack_records(results, self.max_persons).tobytes())
+        """results: this rank's [(frame_id, status, n_peaks, poses, scores)] of one step (whole
+        results: the frames with more persons than a record holds travel as overflow)."""
+        rec = pack_records(results, self.max_persons).tobytes()
+        ovf = pack_full([r for r in results if r[1] == 0 and len(r[4]) > self.max_persons])
+        self.pending.append(struct.pack("<q", len(rec)) + rec + ovf)
 
     def wait(self, timeout=None):
-        """Rank 0: every rank's records of the oldest submitted step, by frame id; else None."""
+        """Rank 0: every rank's whole results of the oldest submitted step, by frame id; else None."""
         got = self.t.gather(self.pending.pop(0))
         if got is None:
             return None
-        return unpack_records(b"".join(got), self.max_persons)
+        recs, ovf = [], []
+        for g in got:
+            (n,) = struct.unpack("<q", g[:8])
+            recs.append(g[8:8 + n])
+            ovf += unpack_full(g[8 + n:])
+        return merge_overflow(unpack_records(b"".join(recs), self.max_persons), ovf)
 
 
 class RcclGather(object):
@@ -240,6 +286,8 @@ class RcclGather(object):
         _lib.check(L.op_comm_create(ctx.h, transport.world, transport.rank, uid, self.timeout, ctypes.byref(h)),
                    "op_comm_create")
         self.h = h
+        self._sub = []  # (frame_base, frame_stride) of the outstanding submits, oldest first
+        self.overflow_s = 0.0  # host time spent re-running this rank's overflow frames
 
     def submit(self, first, n, frame_base, frame_stride):
         """Enqueue the gather of this rank's staged frames [first, first+n) (global ids
@@ -247,18 +295,58 @@ class RcclGather(object):
         self._lib.check(self._lib.lib().op_comm_gather_results(self.h, self.ctx.h, int(first), int(n),
                                                                self.max_persons, int(frame_base),
                                                                int(frame_stride)), "op_comm_gather_results")
+        self._sub.append((int(frame_base), int(frame_stride)))
+
+    def _own_overflow(self, base, stride):
+        """Whole results of this rank's frames of the step just waited for that its records could
+        not carry (op_comm_overflow / op_comm_overflow_result: re-run uncapped on this device)."""
+        ct, lib_, L = self._ct, self._lib, self._lib.lib()
+        cnt = ct.c_int32()
+        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, None, 0, ct.byref(cnt)), "op_comm_overflow")
+        if cnt.value == 0:
+            return []
+        idx = (ct.c_int32 * cnt.value)()
+        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, idx, cnt.value, ct.byref(cnt)), "op_comm_overflow")
+        out = []
+        for i in idx:
+            cap = max(self.max_persons, 64)
+            while True:
+                poses = np.empty((cap, N_JOINTS, 3), np.float64)
+                scores = np.empty(cap, np.float64)
+                res = lib_.OpFrameResult()
+                rc = L.op_comm_overflow_result(self.h, self.ctx.h, int(i), lib_.ptr(poses), lib_.ptr(scores), cap,
+                                               ct.byref(res))
+                if rc == lib_.OP_ERR_CAPACITY and res.n_persons > cap:
+                    cap = res.n_persons
+                    continue
+                break
+            if rc != lib_.OP_OK and rc != res.status:  # a frame status (e.g. the reference's IndexError) travels
+                lib_.check(rc, "op_comm_overflow_result")
+            k = res.n_persons if res.status == 0 else 0
+            out.append((base + int(i) * stride, int(res.status), int(res.n_peaks), poses[:k].copy(), scores[:k].copy()))
+        return out
 
     def wait(self, timeout=None, raw=False):
-        """Rank 0: every rank's records of the oldest submitted step (unpacked, by frame id; or the
-        raw record bytes with raw=True); other ranks: None."""
+        """Rank 0: every rank's whole results of the oldest submitted step (unpacked and merged, by
+        frame id; or (raw record bytes, overflow results) with raw=True); other ranks: None.
+        Collective: every rank calls it once per submit (the overflow exchange is a TCP gather)."""
         ct = self._ct
         p, nf, rb = ct.c_void_p(), ct.c_int32(), ct.c_int64()
         self._lib.check(self._lib.lib().op_comm_wait(self.h, float(timeout or self.timeout), ct.byref(p),
                                                      ct.byref(nf), ct.byref(rb)), "op_comm_wait")
+        base, stride = self._sub.pop(0)
+        t0 = time.perf_counter()
+        own = self._own_overflow(base, stride)
+        self.overflow_s += time.perf_counter() - t0
+        if self.t.world > 1:
+            got = self.t.gather(pack_full(own))
+            ovf = None if got is None else [r for g in got for r in unpack_full(g)]
+        else:
+            ovf = own
         if not p.value:
             return None
         buf = ct.string_at(p.value, nf.value * rb.value)
-        return buf if raw else unpack_records(buf, self.max_persons)
+        return (buf, ovf) if raw else merge_overflow(unpack_records(buf, self.max_persons), ovf)
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

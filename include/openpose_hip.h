@@ -196,8 +196,14 @@ int op_stage_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, in
  * stream into a 2-slot device ring and return.  The next op_run_staged* waits for that copy on the
  * compute stream and makes these frames the staged set, so the upload of step k+1 overlaps the
  * compute of step k (the reference uploads each frame inside __call__, pose_detector.py:496-497).
- * The host buffer must stay untouched until that run has been enqueued. */
+ * The copy may still be reading the host buffer after op_upload_frames and the consuming
+ * op_run_staged* have returned: the buffer must stay unchanged until the copy has completed --
+ * after op_upload_wait, op_synchronize, or any later call that waited for the consuming run. */
 int op_upload_frames(op_ctx* ctx, const uint8_t* frames, int32_t n, int32_t h, int32_t w);
+/* Block until every op_upload_frames copy issued so far has finished reading its host buffer (the
+ * buffers may then be refilled).  No reference counterpart (the reference's uploads are
+ * synchronous, pose_detector.py:496-497). */
+int op_upload_wait(op_ctx* ctx);
 /* Page-locked host memory for op_upload_frames sources. */
 int op_host_alloc(size_t bytes, void** p);
 int op_host_free(void* p);
@@ -254,6 +260,23 @@ int op_profile_reset(op_ctx* ctx);
 /* Which classes op_profile_enable times (bit c = class c; default 0xF = all). */
 int op_profile_classes(op_ctx* ctx, int32_t mask);
 
+/* Launch census of the bf16x3 conv kernels (process-wide, all contexts; counted on the host when a
+ * launch is enqueued, so a replayed hipGraph adds nothing): counts[i] for i < n, then the counts are
+ * zeroed if reset.  Lets a test assert which kernel instantiation a configuration really ran (the
+ * 7x7 tile size is picked per launch shape by a cost model).  No reference counterpart.
+ * Slots: 1..10 = conv_m16_bf16x3<7, NPX> launches with NPX 16-px blocks per wave (640-px raster
+ * tiles at 10), and: */
+#define OP_CENSUS_7X7_SPLITK 11  /* 7x7 launches that split their input chunks (split-K) */
+#define OP_CENSUS_7X7_OTHER 12   /* 7x7 on the conv_big fallback family */
+#define OP_CENSUS_3X3_W48 13     /* conv_m16k_bf16x3<false> on 4 x 48 tiles */
+#define OP_CENSUS_3X3_W32 14     /* conv_m16k_bf16x3<false> on 8 x 32 tiles */
+#define OP_CENSUS_3X3_POOL 15    /* conv_m16k_bf16x3<true> (fused 2x2 max-pool) */
+#define OP_CENSUS_3X3_SPLITK 16  /* conv_m16k launches with split-K */
+#define OP_CENSUS_3X3_BIG 17     /* conv_big_bf16x3<3, ...> (shapes conv_m16k does not take) */
+#define OP_CENSUS_CONV1_PAIR 18  /* conv1_pair_bf16x3 (fused conv1_1 + conv1_2 + pool) */
+#define OP_CENSUS_SLOTS 24
+int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
+
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
 double op_forward_flops(int32_t h, int32_t w);
 
@@ -264,7 +287,8 @@ double op_forward_flops(int32_t h, int32_t w);
  * n_persons, 0}, int64 global frame id (frame_base + i * frame_stride), 8 zero bytes, then
  * max_persons x 18 x 3 f64 poses and max_persons f64 scores (persons past max_persons are not
  * carried; n_persons still counts them; rows past n_persons are zero).  A frame over the batched
- * post-process caps carries status OP_ERR_CAPACITY; its rank fetches it with op_fetch_result. */
+ * post-process caps carries status OP_ERR_CAPACITY (op_fetch_result re-runs it uncapped; in a
+ * gather, op_comm_overflow_result). */
 int op_pack_results(op_ctx* ctx, int32_t first, int32_t n, int32_t max_persons, int64_t frame_base,
                     int32_t frame_stride, void* host_records);
 #define OP_COMM_ID_BYTES 128
@@ -285,6 +309,17 @@ int op_comm_gather_results(op_comm* comm, op_ctx* ctx, int32_t first, int32_t n,
  * OP_ERR_TIMEOUT returned).  Rank 0: *records = n_frames records of rec_bytes each in rank order
  * (valid until the gather two submits later); other ranks: *records = NULL, *n_frames = 0. */
 int op_comm_wait(op_comm* comm, double timeout_s, const void** records, int32_t* n_frames, int64_t* rec_bytes);
+/* Every frame reaches rank 0 whole (pose_detector.py:484-517 returns every frame's poses): after
+ * op_comm_wait, each rank lists the frames of its own part of that gather whose record does not
+ * carry the whole result -- status OP_ERR_CAPACITY (over the batched post-process caps) or more
+ * persons than max_persons -- as indices i in [0, n) of its op_comm_gather_results call (global id
+ * frame_base + i * frame_stride).  Their post-process input was copied aside on the device when the
+ * records were packed, so op_comm_overflow_result re-runs frame i alone (uncapped, big mode: the
+ * result op_fetch_result would have given) even after later steps have run; the host ships those
+ * results to rank 0 (frames.py: TCP).  Valid until the next op_comm_wait. */
+int op_comm_overflow(op_comm* comm, op_ctx* ctx, int32_t* frames, int32_t cap, int32_t* count);
+int op_comm_overflow_result(op_comm* comm, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,
+                            op_frame_result* res);
 
 /* ---- Face / hand keypoint detectors: FaceNet / HandNet single-branch CPM nets ----
  * face_detector.py:12-56 (FaceDetector), hand_detector.py:12-66 (HandDetector); the same conv kernels

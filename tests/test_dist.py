@@ -14,7 +14,7 @@ import pytest
 
 from conftest import REPO, golden_cases, load_golden, pkg_module
 
-MAXP = 8  # smaller than the 20-person golden: records carry the first MAXP persons
+MAXP = 8  # smaller than the 20-person golden: those frames travel whole as overflow
 
 
 def _free_port():
@@ -76,7 +76,8 @@ def test_socket_gather_matches_single_process(world, n_frames):
         assert p.exitcode == 0
     assert mx == world and sm == world
     for s in range(steps):
-        want = F.unpack_records(F.pack_records(_frame_results(range(s * n_frames, (s + 1) * n_frames)), MAXP), MAXP)
+        want = _frame_results(range(s * n_frames, (s + 1) * n_frames))  # every frame whole
+        assert any(len(w[4]) > MAXP for w in want)  # some frames hold more persons than a record carries
         assert [r[0] for r in got[s]] == list(range(s * n_frames, (s + 1) * n_frames))
         for a, b in zip(got[s], want):
             assert a[:3] == b[:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
@@ -137,3 +138,21 @@ def test_count_persons_reads_exact_header_counts():
     buf = F.pack_records(recs, 4).tobytes()
     want = sum(len(r[4]) for r in recs if r[1] == 0)
     assert F.count_persons(buf, 4) == (want, 1)
+
+
+def test_count_persons_and_merge_with_overflow():
+    """A record over the batched caps (status 3, no persons) is counted from its overflow result;
+    without one it counts as undelivered.  Records past max_persons keep their exact header count."""
+    F = pkg_module("frames")
+    res = _frame_results(range(4))
+    rec = [(fid, st, npk, p, s) for fid, st, npk, p, s in res]
+    rec[2] = (rec[2][0], F.STATUS_CAPACITY, rec[2][2], np.zeros((0, 18, 3)), np.zeros(0))
+    buf = F.pack_records(rec, MAXP).tobytes()
+    total = sum(len(r[4]) for r in res)
+    assert F.count_persons(buf, MAXP, [res[2]]) == (total, 0)
+    assert F.count_persons(buf, MAXP) == (total - len(res[2][4]), 1)
+    merged = F.merge_overflow(F.unpack_records(buf, MAXP), [res[2]])
+    assert merged[2][1] == 0 and np.array_equal(merged[2][4], res[2][4])
+    back = F.unpack_full(F.pack_full(res))
+    for a, b in zip(back, res):
+        assert a[:3] == b[:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])

@@ -133,3 +133,27 @@ def test_updater_schedule_and_loss_decreases():
     g = up.grads()
     assert not g["conv1_1"][0].any() and g["conv4_3_CPM"][0].any()  # VGG frozen until iteration 2000
     up.ctx.close()
+
+
+@pytest.mark.parametrize("case", ["posenet_2x48x48", "posenet_1x64x80"])
+def test_train_step_losses_vs_reference_compute_loss(case):
+    """op_train_step's twelve per-stage losses against the REFERENCE's own compute_loss
+    (train_coco_pose_estimation.py:41-73, tests/golden/train/, made by make_golden_train.py) on the
+    reference network's own stage outputs for the same weights (seed 0) and input.  The device
+    recomputes the forward itself (exact f32), so the losses agree to the forward's 1e-3-level map
+    agreement, far tighter in relative terms: rtol 1e-4."""
+    from test_train_golden import load_train_case
+    from test_forward_golden import case_weights, load_case
+    lib = pkg_module("_lib")
+    g, _ = load_train_case(case)
+    _, d = load_case(case)
+    n, h, w = d["x"].shape[0], d["x"].shape[2], d["x"].shape[3]
+    ctx = lib.TrainContext(n, h, w, 0)
+    try:
+        ctx.set_weights(case_weights("posenet", 0))
+        losses = ctx.step(d["x"], g["pafs_t"], g["heatmaps_t"], g["ignore_mask"])
+    finally:
+        ctx.close()
+    want = np.stack([g["paf_loss"], g["heat_loss"]], 1).reshape(-1)  # [paf, heat] per stage
+    print(case, "max rel loss error vs reference compute_loss: %.3g" % float(np.max(np.abs(losses - want) / want)))
+    np.testing.assert_allclose(losses, want, rtol=1e-4)
