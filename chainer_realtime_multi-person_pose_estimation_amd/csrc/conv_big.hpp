@@ -86,6 +86,10 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
 int launch_m16k_wide(dim3 grid, int lds, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                      const SplitConvGroup& g1, const BigTiling& tl);
 
+// conv_m16r.hip: the register-weight, double-buffered-halo 3x3 kernel (large launches); *taken = 0
+// when the shape or launch size is outside it
+int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool, hipStream_t st, int* taken);
+
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl);
 

@@ -1,0 +1,316 @@
+// conv_m16r_bf16x3: 3x3 convs on v_mfma_f32_16x16x32_bf16 with register-resident weights and a
+// double-buffered LDS halo (round 3; the default 3x3 kernel where the launch is large enough).
+//
+// Same arithmetic as conv_m16k_bf16x3 (conv_m16k.hpp): K = 32 of one MFMA is one tap over a PAIR of
+// 16-channel input chunks (lane group g = lane / 16: chunk g / 2, channel half g % 2), three bf16
+// products per f32-accurate MAC (hi*hi, hi*lo, lo*hi), accumulated per output in the order (chunk
+// pair, tap, hi*hi, hi*lo, lo*hi) -- so every output is BIT-IDENTICAL to conv_m16k's.  What changes
+// is where the operands come from:
+//
+// * A (weights): each wave owns 32 output channels and loads their fragments for a step straight
+//   from global memory (L2) into VGPRs, two steps ahead -- no shared weight ring in LDS, so no
+//   LDS-DMA staging of weights, no A reads from LDS and no workgroup barrier per tap (conv_m16k
+//   pays all three every step: weight staging and the per-step barrier were ~8.5 % of its time in
+//   round 2's traffic experiments).
+// * B (pixels): every wave of the workgroup covers the SAME pixel tile (TR rows x 16*TCB columns),
+//   read from an LDS halo of both chunks of the pair (8 planes of 16 B per pixel, tight pitch,
+//   compile-time tap offsets: one ds_read_b128 with an immediate offset per fragment).  The halo is
+//   double-buffered: the next chunk pair's halo is streamed in by LDS-DMA during taps 0..4 of the
+//   current pair, so the once-per-pair reload (~10 % of conv_m16k's time) leaves the critical path;
+//   one workgroup barrier per chunk pair swaps the buffers.
+//
+// NW waves x 32 channels = the workgroup's channel tile (NW = 8: 256 channels, one workgroup per
+// CU; NW = 4: 128 channels, two per CU).  POOL: fused 2x2 max-pool epilogue (tile rows r, r + 1 =
+// blocks pb, pb + TCB; columns = lanes l, l ^ 1).  Layer semantics: models/CocoPoseNet.py:136-163
+// (conv + ReLU, the pools after conv1_2 / conv2_2 / conv3_4).
+#include "conv_big.hpp"
+
+namespace op {
+
+// LDS-DMA from inline asm: invisible to the compiler's waitcnt pass, so the B-fragment reads of the
+// current buffer do not wait for the next buffer's pieces (with the builtin the pass cannot tell the
+// two apart and would serialise them).  Writes M0; nothing else in this kernel uses M0.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory");
+}
+
+template <int NW, int TCB, int TR, bool POOL>
+__global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s, SplitConvGroup g0,
+                                                                   SplitConvGroup g1, BigTiling tl) {
+  constexpr int NPX = TR * TCB;           // 16-px blocks per wave (the whole pixel tile)
+  constexpr int TC = 16 * TCB;
+  constexpr int PITCH = TC + 2;
+  constexpr int HROWS = TR + 2;
+  constexpr int NH = (HROWS * PITCH + 63) / 64;  // 1-KiB pieces per halo plane
+  constexpr int HPLANE = NH * 1024;
+  constexpr int HBUF = 8 * HPLANE;               // 2 chunks x 4 planes (hi/lo x 2 channel halves)
+  constexpr int PIECES = 8 * NH / NW;            // halo pieces per wave per chunk pair
+  constexpr int HSTEPS = 5;                      // taps during which the next pair's halo is issued
+  constexpr int PPS = (PIECES + HSTEPS - 1) / HSTEPS;
+  constexpr int CW = NW * 32;
+  static_assert((8 * NH) % NW == 0, "halo pieces split evenly over the waves");
+  static_assert(!POOL || (TR % 2 == 0), "pooled tiles hold whole row pairs");
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [2][8 planes][NH KiB]
+
+  const int lin = blockIdx.x;
+  int unit, widx;
+  if (tl.xpu) {
+    const int xcd = lin & 7, slot = lin >> 3;
+    unit = xcd / tl.xpu;
+    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
+  } else {
+    unit = lin / tl.per_unit;
+    widx = lin - unit * tl.per_unit;
+  }
+  if (unit >= tl.units || widx >= tl.per_unit) return;
+  const int grp = unit / tl.co_tiles;
+  const int co0 = (unit - grp * tl.co_tiles) * CW;
+  const SplitConvGroup g = grp == 0 ? g0 : g1;
+  if (co0 >= g.cop) return;
+  const int tpf = tl.tiles_y * tl.tiles_x;
+  const int frame = widx / tpf;
+  const int tix = widx - frame * tpf;
+  const int ty = tix / tl.tiles_x;
+  const int y0 = ty * TR, x0 = (tix - ty * tl.tiles_x) * TC;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, kg = lane >> 4;
+  const int csel = kg >> 1, khalf = kg & 1;
+  const int wp_in = s.w + 2 * s.pin;
+  const int hp_in = s.h + 2 * s.pin;
+  const int64_t pix_bytes = (int64_t)s.cs_in * 4;
+  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)lds;
+
+  // ---- A: this wave's 32 channels; weights [c16][tap][plane 2*khalf + hi/lo][cop][8 bf16] ----
+  const int64_t wplane = (int64_t)g.cop * 16;
+  const int cw0 = co0 + wave * 32;
+  const char* const wlane = (const char*)g.w + ((int64_t)csel * 9 * 4 + 2 * khalf) * wplane + (int64_t)(cw0 + l16) * 16;
+  const int ncp = s.c16 / 2;
+  const int n_it = ncp * 9;
+  typedef bf16x8g AFrag[4];  // [cb * 2 + hl]
+  AFrag abuf[3];
+  auto load_a = [&](int it, AFrag& a) {
+    if (it >= n_it) it = n_it - 1;  // the last steps' prefetch re-reads the final step (unused)
+    const int cp = it / 9, t = it - cp * 9;
+    const char* p = wlane + (int64_t)((2 * cp * 9 + t) * 4) * wplane;
+    a[0] = *(const bf16x8g*)p;
+    a[1] = *(const bf16x8g*)(p + wplane);
+    a[2] = *(const bf16x8g*)(p + 256);
+    a[3] = *(const bf16x8g*)(p + wplane + 256);
+  };
+
+  // ---- B: halo of one chunk pair; wave w DMAs pieces j = w, w + NW, ... (plane j / NH, piece j % NH) ----
+  auto halo_piece = [&](int cp, int buf, int k) {  // k-th of this wave's PIECES pieces
+    const int j = wave + k * NW;
+    const int plane = j / NH, i = j - (j / NH) * NH;
+    const int cj = plane >> 2, pl = plane & 3;
+    const int slot = i * 64 + lane;
+    const int hr = slot / PITCH, hc = slot - (slot / PITCH) * PITCH;
+    const int yy = min(y0 - 1 + hr + s.pin, hp_in - 1), xx = min(x0 - 1 + hc + s.pin, wp_in - 1);
+    const char* src = fbase + (int64_t)(yy * wp_in + xx) * pix_bytes + (2 * cp + cj) * 64 + pl * 16;
+    dma16(src, lds0 + (uint32_t)(buf * HBUF + plane * HPLANE + i * 1024));
+  };
+
+  const int rows_here = min(TR, s.h - y0);
+  const int cols_here = min(TC, s.w - x0);
+  // this lane's halo byte offset within a buffer: plane of (chunk csel, half khalf, hi), pixel l16
+  const int bl0 = (csel * 4 + 2 * khalf) * HPLANE + l16 * 16;
+
+  floatx4 acc[2][NPX];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: chunk pair 0's halo into buffer 0, the first two steps' weights
+#pragma unroll
+  for (int k = 0; k < PIECES; ++k) halo_piece(0, 0, k);
+  load_a(0, abuf[0]);
+  load_a(1, abuf[1]);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int cp = 0; cp < ncp; ++cp) {
+    const int buf = cp & 1;
+    const char* const hb = lds + buf * HBUF + bl0;
+    const bool next = cp + 1 < ncp;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int it = cp * 9 + t;
+      load_a(it + 2, abuf[(t + 2) % 3]);  // two steps ahead (it % 3 == t % 3: 9 taps per pair)
+      if (t < HSTEPS && next) {
+#pragma unroll
+        for (int k = t * PPS; k < (t + 1) * PPS && k < PIECES; ++k) halo_piece(cp + 1, buf ^ 1, k);
+      }
+      const AFrag& a = abuf[t % 3];
+      const int toff = ((t / 3) * PITCH + (t % 3)) * 16;
+      bf16x8g bh[2], bl[2];
+      bh[0] = *(const bf16x8g*)(hb + toff);
+      bl[0] = *(const bf16x8g*)(hb + toff + HPLANE);
+#pragma unroll
+      for (int pb = 0; pb < NPX; ++pb) {
+        const int cur = pb & 1;
+        if (pb + 1 < NPX) {
+          const int q1 = ((pb + 1) / TCB) * PITCH + ((pb + 1) % TCB) * 16;
+          bh[cur ^ 1] = *(const bf16x8g*)(hb + toff + q1 * 16);
+          bl[cur ^ 1] = *(const bf16x8g*)(hb + toff + q1 * 16 + HPLANE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh[cur], acc[cb][pb], 0, 0, 0);
+        }
+      }
+    }
+    if (next) {
+      // this wave's pieces of the next pair were issued by tap 4; younger than them are only the
+      // weight loads of taps 5..8 (4 each): waiting down to 8 outstanding covers every piece
+      wait_vmcnt<8>();
+      __builtin_amdgcn_s_barrier();  // every wave's pieces landed; this pair's buffer is free
+      asm volatile("" ::: "memory");
+    }
+  }
+  wait_vmcnt<0>();
+
+  if constexpr (POOL) {
+    const int wp_out = s.w / 2 + 2 * s.pout;
+    const int hp_out = s.h / 2 + 2 * s.pout;
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      if ((pb / TCB) & 1) continue;  // odd tile rows are the pair partners
+      const int r = pb / TCB, c = (pb % TCB) * 16 + l16;
+      const int y = y0 + r, x = x0 + c;
+      const bool store = r < rows_here && c < cols_here && (l16 & 1) == 0;
+      char* optr = (char*)g.out +
+                   ((int64_t)(frame * hp_out + y / 2 + s.pout) * wp_out + (x / 2 + s.pout)) * (int64_t)s.cs_out * 4;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int co = cw0 + cb * 16 + 4 * kg;
+        const bool live = co < g.cout_store;
+        const floatx4 bv = live ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f};
+        u16x4g vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float m = 0.0f;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            float f = acc[cb][pb + k * TCB][e] + bv[e];
+            if (s.relu) f = f > 0.0f ? f : 0.0f;
+            const __bf16 h16 = (__bf16)f;
+            const float rc = (float)h16 + (float)(__bf16)(f - (float)h16);
+            m = k == 0 ? rc : fmaxf(m, rc);
+          }
+          m = fmaxf(m, __shfl_xor(m, 1));
+          const __bf16 h16 = (__bf16)m;
+          const __bf16 l16v = (__bf16)(m - (float)h16);
+          vh[e] = __builtin_bit_cast(unsigned short, h16);
+          vl[e] = __builtin_bit_cast(unsigned short, l16v);
+        }
+        if (store && live) {
+          char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+          *(u16x4g*)d = vh;
+          *(u16x4g*)(d + 16) = vl;
+        }
+      }
+    }
+    return;
+  }
+
+  const int wp_out = s.w + 2 * s.pout;
+  const int hp_out = s.h + 2 * s.pout;
+#pragma unroll
+  for (int pb = 0; pb < NPX; ++pb) {
+    const int r = pb / TCB, c = (pb % TCB) * 16 + l16;
+    const bool live = r < rows_here && c < cols_here;
+    const int y = y0 + r, x = x0 + c;
+    char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
+    float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int co = cw0 + cb * 16 + 4 * kg;
+      floatx4 v;
+      uint32_t own[4], w[4];
+      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu, v,
+                      own, w);
+      if (!live || co >= g.cout_store) continue;
+      store_split_group(optr, co, kg, g.cout_store, own, w);
+      if (o32) *(floatx4*)(o32 + co) = v;
+    }
+  }
+}
+
+template <int NW, int TCB, int TR, bool POOL>
+static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const SplitConvGroup& g1, const BigTiling& tl,
+                    hipStream_t st) {
+  constexpr int PITCH = 16 * TCB + 2;
+  constexpr int NH = ((TR + 2) * PITCH + 63) / 64;
+  constexpr int LDS = 2 * 8 * NH * 1024;
+  static_assert(LDS <= 160 * 1024 / (8 / NW), "workgroups per CU x LDS fits 160 KiB");
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16r_bf16x3<NW, TCB, TR, POOL>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
+    attr = true;
+  }
+  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+                                 : (unsigned)(tl.units * tl.per_unit);
+  hipLaunchKernelGGL((conv_m16r_bf16x3<NW, TCB, TR, POOL>), dim3(blocks), dim3(NW * 64), LDS, st, s, g0, g1, tl);
+  return OP_OK;
+}
+
+// Tiling + launch of conv_m16r_bf16x3 for a 3x3 split-format conv; *taken = 0 when the shape is
+// outside it (the caller falls back to conv_m16k / conv_big).  mode: OP_M16R (0 off, 1 auto: 256
+// channels per workgroup where Co is a multiple of 256, else 128; 4 / 8 force NW).
+int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool, hipStream_t st, int* taken) {
+  *taken = 0;
+  static const int mode = getenv("OP_M16R") ? atoi(getenv("OP_M16R")) : 1;
+  if (!mode || s.ks != 3 || s.pin < 1 || s.cs_in % 16 || (s.c16 & 1) || s.halo_mode != 4) return OP_OK;
+  int cop_max = 0;
+  for (int i = 0; i < s.groups; ++i) {
+    if (g[i].cop % 128 || g[i].cin_off % 16) return OP_OK;
+    cop_max = std::max(cop_max, g[i].cop);
+  }
+  if (pool && (s.groups != 1 || (s.h & 1) || (s.w & 1) || !s.relu)) return OP_OK;
+  int nw = (mode == 4 || mode == 8) ? mode : 4;
+  if (mode == 1) {
+    bool all256 = true;
+    for (int i = 0; i < s.groups; ++i) all256 = all256 && g[i].cop % 256 == 0;
+    nw = all256 ? 8 : 4;
+  }
+  if (nw == 8)
+    for (int i = 0; i < s.groups; ++i)
+      if (g[i].cop % 256) return OP_OK;
+  // 4 x 48 tiles: 46- / 92- / 184-wide maps at 96 % column use
+  constexpr int TCB = 3, TR = 4;
+  BigTiling t{};
+  t.tc = 16 * TCB;
+  t.tr = TR;
+  t.tiles_x = (s.w + t.tc - 1) / t.tc;
+  t.tiles_y = (s.h + TR - 1) / TR;
+  t.co_tiles = cop_max / (nw * 32);
+  t.units = s.groups * t.co_tiles;
+  t.per_unit = s.n * t.tiles_y * t.tiles_x;
+  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  // enough workgroups to fill the chip several times; small launches keep conv_m16k (split-K)
+  const int64_t wgs = (int64_t)t.units * t.per_unit;
+  if (wgs < (nw == 8 ? 2 * 256 : 4 * 256)) return OP_OK;
+  *taken = 1;
+  const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+  census_add(pool ? OP_CENSUS_3X3_R_POOL : nw == 8 ? OP_CENSUS_3X3_R256 : OP_CENSUS_3X3_R128);
+  int rc;
+  if (nw == 8)
+    rc = pool ? launch_t<8, TCB, TR, true>(s, g[0], g1, t, st) : launch_t<8, TCB, TR, false>(s, g[0], g1, t, st);
+  else
+    rc = pool ? launch_t<4, TCB, TR, true>(s, g[0], g1, t, st) : launch_t<4, TCB, TR, false>(s, g[0], g1, t, st);
+  if (rc != OP_OK) return rc;
+  OP_AFTER_LAUNCH("conv_m16r_bf16x3", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+}  // namespace op

@@ -274,6 +274,9 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_3X3_SPLITK 16  /* conv_m16k launches with split-K */
 #define OP_CENSUS_3X3_BIG 17     /* conv_big_bf16x3<3, ...> (shapes conv_m16k does not take) */
 #define OP_CENSUS_CONV1_PAIR 18  /* conv1_pair_bf16x3 (fused conv1_1 + conv1_2 + pool) */
+#define OP_CENSUS_3X3_R256 19    /* conv_m16r_bf16x3<8, ...> (register weights, 256 channels per workgroup) */
+#define OP_CENSUS_3X3_R128 20    /* conv_m16r_bf16x3<4, ...> (128 channels per workgroup) */
+#define OP_CENSUS_3X3_R_POOL 21  /* conv_m16r_bf16x3<., ., ., true> (fused 2x2 max-pool) */
 #define OP_CENSUS_SLOTS 24
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

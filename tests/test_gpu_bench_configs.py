@@ -111,6 +111,9 @@ def test_staged_u8_path_at_the_headline_batch(lib, bctx):
             pinned.close()
         assert set(cen["npx"]) == {10} and cen["npx"][10] == 25, cen
         assert cen["conv1_pair"] == 1 and cen["3x3_splitk"] == 0, cen
+        # the register-weight 3x3 kernel runs the large 3x3 launches of this batch (bit-identical to
+        # conv_m16k, which the single-frame runs below take: asserted by the per-frame comparison)
+        assert cen["3x3_r256"] + cen["3x3_r128"] + cen["3x3_r_pool"] >= 8, cen
         assert paf.shape == (n, 38, 46, 46) and heat.shape == (n, 19, 46, 46)
         # a border-spanning frame in the middle, and the two ends, against the CPU oracle
         W = case_weights("posenet", 0)
