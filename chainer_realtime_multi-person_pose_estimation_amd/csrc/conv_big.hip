@@ -761,12 +761,12 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
       g[0].cin_off % 16 || !s.relu)
     return OP_OK;
   const bool c128 = g[0].cop % 128 == 0;
-  if (c128) {
-    const int rc = launch_conv_m16r(s, g, true, st, taken);
-    if (rc != OP_OK || *taken) return rc;
-  }
   BigTiling t{};
   if (c128 && m16k_tiling(s, 1, g[0].cop, true, t)) {
+    // large launches of the shapes conv_m16k takes run the register-weight kernel instead: the
+    // same accumulation order, so a frame's result does not depend on which of the two ran
+    const int rc = launch_conv_m16r(s, g, true, st, taken);
+    if (rc != OP_OK || *taken) return rc;
     *taken = 1;
     return launch_m16k(s, g, t, true, st);
   }
@@ -906,9 +906,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
     return launch_big_t<7, 6, 8, 128, 1>(s, g, tl, st);
   }
   if (c128) {
-    const int rc = launch_conv_m16r(s, g, false, st, taken);
-    if (rc != OP_OK || *taken) return rc;
     if (m16k_tiling(s, s.groups, cop_max, false, tl)) {
+      const int rc = launch_conv_m16r(s, g, false, st, taken);  // large launches (same order, above)
+      if (rc != OP_OK || *taken) return rc;
       if (plain_order) tl.xpu = 0;
       *taken = 1;
       return launch_m16k(s, g, tl, false, st);

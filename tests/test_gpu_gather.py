@@ -23,6 +23,11 @@ def _host_records(F, ctx, n, base, stride):
     return F.pack_records([(base + i * stride, r.status, r.n_peaks, p, s) for i, (p, s, r) in enumerate(res)], MAXP)
 
 
+def _host_results(ctx, n, base, stride):
+    """Whole results (what RcclGather.wait delivers: records merged with the overflow frames)."""
+    return [(base + i * stride, r.status, r.n_peaks, p, s) for i, (p, s, r) in enumerate(ctx.fetch_results(0, n))]
+
+
 def test_device_records_equal_host_records(ctx, lib):
     F = pkg_module("frames")
     _staged(ctx, 3)
@@ -46,18 +51,18 @@ def test_rccl_gather_one_rank_double_buffered(ctx):
         ctx.run_staged()
         g.submit(0, 2, 0, 1)           # step 0's gather (async, behind step 0's post-process)
         ctx.synchronize()
-        want0 = F.unpack_records(_host_records(F, ctx, 2, 0, 1), MAXP)
+        want0 = _host_results(ctx, 2, 0, 1)
         ctx.run_staged(graph=True)     # step 1 overlaps step 0's gather
         g.submit(0, 2, 2, 1)
         got0 = g.wait()
         ctx.synchronize()
-        want1 = F.unpack_records(_host_records(F, ctx, 2, 2, 1), MAXP)
+        want1 = _host_results(ctx, 2, 2, 1)
         got1 = g.wait()
         for got, want in ((got0, want0), (got1, want1)):
             assert [r[0] for r in got] == [r[0] for r in want]
             for a, b in zip(got, want):
                 assert a[1:3] == b[1:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
-        assert got0[0][2] > 0 and len(got0[0][4]) == MAXP
+        assert got0[0][2] > 0 and len(got0[0][4]) > MAXP  # whole: more persons than a record carries
         with pytest.raises(RuntimeError):
             g.wait()  # nothing outstanding
     finally:
