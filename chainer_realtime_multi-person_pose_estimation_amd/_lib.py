@@ -130,7 +130,7 @@ def lib():
         "op_comm_destroy": ([P], ctypes.c_int),
         "op_comm_gather_results": ([P, P, I32, I32, I32, ctypes.c_int64, I32], ctypes.c_int),
         "op_comm_wait": ([P, ctypes.c_double, P, P, P], ctypes.c_int),
-        "op_comm_overflow": ([P, P, P, I32, P], ctypes.c_int),
+        "op_comm_overflow": ([P, P, P, P, I32, P], ctypes.c_int),
         "op_comm_overflow_result": ([P, P, I32, P, P, I32, P], ctypes.c_int),
         "op_upload_frames": ([P, P, I32, I32, I32], ctypes.c_int),
         "op_upload_wait": ([P], ctypes.c_int),

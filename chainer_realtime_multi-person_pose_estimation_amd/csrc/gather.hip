@@ -24,7 +24,7 @@
 extern "C" int64_t record_bytes(int max_persons);
 extern "C" int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame_base, int frame_stride,
                                 void* dst, hipStream_t* stream, int keep_slot);
-extern "C" int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t cap, int32_t* count);
+extern "C" int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count);
 extern "C" int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* scores, int32_t cap,
                                op_frame_result* res);
 extern "C" int ctx_device(op_ctx* c);
@@ -276,7 +276,7 @@ int op_comm_wait(op_comm* g, double timeout_s, const void** records, int32_t* n_
   return OP_OK;
 }
 
-int op_comm_overflow(op_comm* g, op_ctx* ctx, int32_t* frames, int32_t cap, int32_t* count) {
+int op_comm_overflow(op_comm* g, op_ctx* ctx, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count) {
   if (!g || !ctx || !count) {
     set_error("op_comm_overflow: bad arguments");
     return OP_ERR_INVALID;
@@ -285,7 +285,7 @@ int op_comm_overflow(op_comm* g, op_ctx* ctx, int32_t* frames, int32_t cap, int3
     set_error("op_comm_overflow: no gather waited for yet");
     return OP_ERR_STATE;
   }
-  return ctx_kept_overflow(ctx, g->last, frames, cap, count);
+  return ctx_kept_overflow(ctx, g->last, frames, reasons, cap, count);
 }
 
 int op_comm_overflow_result(op_comm* g, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,

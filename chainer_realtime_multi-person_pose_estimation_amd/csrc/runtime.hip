@@ -232,9 +232,12 @@ struct PostRecord {
 struct KeepSlot {
   float* maps = nullptr;
   size_t maps_cap = 0;  // bytes
+  double* res = nullptr;  // frames past max_persons: their batched result rows [frame][maxs][54 + 1]
+  size_t res_cap = 0;
+  int maxs = 0;
   int32_t* cnt = nullptr;
   size_t cnt_cap = 0;
-  int32_t* d_hdr = nullptr;  // n x {status, n_peaks, n_persons, flagged}
+  int32_t* d_hdr = nullptr;  // n x {status, n_peaks, n_persons, why: 0 whole record, 1 over the caps, 2 > max_persons}
   int32_t* h_hdr = nullptr;  // pinned copy, complete when the slot's gather is
   size_t hdr_cap = 0;
   PostRecord rec{};
@@ -1302,6 +1305,7 @@ int op_destroy(op_ctx* c) {
   if (c->up_pinned) hipHostFree(c->up_pinned);
   for (auto& k : c->keep) {
     if (k.maps) hipFree(k.maps);
+    if (k.res) hipFree(k.res);
     if (k.cnt) hipFree(k.cnt);
     if (k.d_hdr) hipFree(k.d_hdr);
     if (k.h_hdr) hipHostFree(k.h_hdr);
@@ -2240,23 +2244,32 @@ __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, in
 
 int64_t record_bytes(int max_persons) { return 32 + (int64_t)max_persons * 55 * 8; }
 
-// Keep slot fill (see KeepSlot): per frame, its header and whether the record cannot carry the
-// whole result; for those frames, the recorded post-process input and batched peak counts.
+// Keep slot fill (see KeepSlot): per frame, its header and why its record cannot carry the whole
+// result.  A frame over the batched caps keeps its post-process input and batched peak counts (it
+// is re-run alone in big mode); a frame with more persons than the record holds keeps its batched
+// result rows (they are complete: copied out as they are).
 __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, int max_persons, const float* __restrict__ src,
                                                      int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
-                                                     int32_t* __restrict__ hdr) {
+                                                     double* __restrict__ res, int32_t* __restrict__ hdr) {
   const int i = blockIdx.x;
   const int f = first + i;
   const int status = b.res_hdr[4 * f];
   const int persons = b.res_hdr[4 * f + 2];
-  const int flag = status == OP_ERR_CAPACITY || (status == OP_OK && persons > max_persons);
+  const int why = status == OP_ERR_CAPACITY ? 1 : (status == OP_OK && persons > max_persons) ? 2 : 0;
   if (threadIdx.x == 0) {
     hdr[4 * i] = status;
     hdr[4 * i + 1] = b.res_hdr[4 * f + 1];
     hdr[4 * i + 2] = status == OP_OK ? persons : 0;
-    hdr[4 * i + 3] = flag;
+    hdr[4 * i + 3] = why;
   }
-  if (!flag || !src) return;
+  if (why == 2) {
+    const double* ps = b.res_poses + (int64_t)f * b.maxs * 54;
+    double* d = res + (int64_t)i * b.maxs * 55;
+    for (int e = threadIdx.x; e < persons * 54; e += 256) d[e] = ps[e];
+    for (int e = threadIdx.x; e < persons; e += 256) d[(int64_t)b.maxs * 54 + e] = b.res_scores[(int64_t)f * b.maxs + e];
+    return;
+  }
+  if (why != 1 || !src) return;
   if (threadIdx.x < OP_N_JOINTS) cnt[i * OP_N_JOINTS + threadIdx.x] = b.peak_cnt[f * OP_N_JOINTS + threadIdx.x];
   const float* s = src + (int64_t)f * fstride;
   float* d = dst + (int64_t)i * fstride;
@@ -2284,6 +2297,8 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)n * fstride * 4, "keep_maps"));
       RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)n * OP_N_JOINTS * 4, "keep_cnt"));
     }
+    RC(grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)n * c->pb.maxs * 55 * 8, "keep_res"));
+    k.maxs = c->pb.maxs;
     const size_t hb = (size_t)n * 16;
     if (hb > k.hdr_cap) {
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
@@ -2297,7 +2312,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.hdr_cap = hb;
     }
     hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                       k.maps, k.cnt, k.d_hdr);
+                       k.maps, k.cnt, k.res, k.d_hdr);
     OP_AFTER_LAUNCH("keep_overflow", c->stream);
     OP_HIP_CHECK(hipMemcpyAsync(k.h_hdr, k.d_hdr, hb, hipMemcpyDeviceToHost, c->stream));
     k.rec = r;
@@ -2314,7 +2329,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
 
 // This rank's frames (slot-relative) of keep slot `slot` whose record does not carry the whole
 // result; valid once the slot's gather has completed (op_comm_wait).
-int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t cap, int32_t* count) {
+int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count) {
   if (slot < 0 || slot > 1 || !count || (cap > 0 && !frames)) {
     set_error("kept overflow: bad arguments");
     return OP_ERR_INVALID;
@@ -2323,7 +2338,10 @@ int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t cap, int32_t
   int m = 0;
   for (int i = 0; i < k.n; ++i)
     if (k.h_hdr[4 * i + 3]) {
-      if (m < cap) frames[m] = i;
+      if (m < cap) {
+        frames[m] = i;
+        if (reasons) reasons[m] = k.h_hdr[4 * i + 3];
+      }
       ++m;
     }
   *count = m;
@@ -2341,6 +2359,20 @@ int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* score
   if (!k.h_hdr[4 * frame + 3]) {
     set_error("kept result: the frame's record carries its whole result");
     return OP_ERR_STATE;
+  }
+  if (k.h_hdr[4 * frame + 3] == 2) {  // complete batched rows, kept as they were
+    const int p = k.h_hdr[4 * frame + 2];
+    res->status = OP_OK;
+    res->n_peaks = k.h_hdr[4 * frame + 1];
+    res->n_persons = p;
+    if (p > cap) {
+      set_error("result capacity too small");
+      return OP_ERR_CAPACITY;
+    }
+    const double* d = k.res + (size_t)frame * k.maxs * 55;
+    OP_HIP_CHECK(hipMemcpy(poses, d, (size_t)p * 54 * 8, hipMemcpyDeviceToHost));
+    OP_HIP_CHECK(hipMemcpy(scores, d + (size_t)k.maxs * 54, (size_t)p * 8, hipMemcpyDeviceToHost));
+    return OP_OK;
   }
   if (k.rec.kind == 0) {
     set_error("kept result: no recorded post-process input for this slot");

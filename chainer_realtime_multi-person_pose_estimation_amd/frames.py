@@ -287,7 +287,8 @@ class RcclGather(object):
                    "op_comm_create")
         self.h = h
         self._sub = []  # (frame_base, frame_stride) of the outstanding submits, oldest first
-        self.overflow_s = 0.0  # host time spent re-running this rank's overflow frames
+        self.overflow_s = 0.0  # host time spent on this rank's overflow frames (re-runs, row copies)
+        self.overflow_caps = 0  # of them, frames over the batched caps (re-run uncapped)
 
     def submit(self, first, n, frame_base, frame_stride):
         """Enqueue the gather of this rank's staged frames [first, first+n) (global ids
@@ -302,11 +303,13 @@ class RcclGather(object):
         not carry (op_comm_overflow / op_comm_overflow_result: re-run uncapped on this device)."""
         ct, lib_, L = self._ct, self._lib, self._lib.lib()
         cnt = ct.c_int32()
-        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, None, 0, ct.byref(cnt)), "op_comm_overflow")
+        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, None, None, 0, ct.byref(cnt)), "op_comm_overflow")
         if cnt.value == 0:
             return []
         idx = (ct.c_int32 * cnt.value)()
-        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, idx, cnt.value, ct.byref(cnt)), "op_comm_overflow")
+        why = (ct.c_int32 * cnt.value)()
+        lib_.check(L.op_comm_overflow(self.h, self.ctx.h, idx, why, cnt.value, ct.byref(cnt)), "op_comm_overflow")
+        self.overflow_caps += sum(1 for w in why if w == 1)
         out = []
         for i in idx:
             cap = max(self.max_persons, 64)

@@ -316,11 +316,13 @@ int op_comm_wait(op_comm* comm, double timeout_s, const void** records, int32_t*
  * op_comm_wait, each rank lists the frames of its own part of that gather whose record does not
  * carry the whole result -- status OP_ERR_CAPACITY (over the batched post-process caps) or more
  * persons than max_persons -- as indices i in [0, n) of its op_comm_gather_results call (global id
- * frame_base + i * frame_stride).  Their post-process input was copied aside on the device when the
- * records were packed, so op_comm_overflow_result re-runs frame i alone (uncapped, big mode: the
- * result op_fetch_result would have given) even after later steps have run; the host ships those
- * results to rank 0 (frames.py: TCP).  Valid until the next op_comm_wait. */
-int op_comm_overflow(op_comm* comm, op_ctx* ctx, int32_t* frames, int32_t cap, int32_t* count);
+ * frame_base + i * frame_stride), with reasons[i] (may be NULL) = 1 over the caps, 2 past
+ * max_persons.  When the records were packed, an over-cap frame's post-process input was copied
+ * aside on the device (op_comm_overflow_result re-runs it alone, uncapped: the result
+ * op_fetch_result would have given) and a frame past max_persons kept its complete result rows
+ * (copied out as they are) -- so both are exact even after later steps have run; the host ships
+ * them to rank 0 (frames.py: TCP).  Valid until the next op_comm_wait. */
+int op_comm_overflow(op_comm* comm, op_ctx* ctx, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count);
 int op_comm_overflow_result(op_comm* comm, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,
                             op_frame_result* res);
 
