@@ -25,6 +25,10 @@
 // (conv + ReLU, the pools after conv1_2 / conv2_2 / conv3_4).
 #include "conv_big.hpp"
 
+#ifndef M16R_FLAT
+#define M16R_FLAT 1  // B fragments pipelined across tap boundaries (0: per tap, as conv_m16k)
+#endif
+
 namespace op {
 
 // LDS-DMA from inline asm: invisible to the compiler's waitcnt pass, so the B-fragment reads of the
@@ -137,6 +141,11 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
     const int buf = cp & 1;
     const char* const hb = lds + buf * HBUF + bl0;
     const bool next = cp + 1 < ncp;
+#if M16R_FLAT
+    bf16x8g bh[2], bl[2];
+    bh[0] = *(const bf16x8g*)hb;
+    bl[0] = *(const bf16x8g*)(hb + HPLANE);
+#endif
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int it = cp * 9 + t;
@@ -146,6 +155,27 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
         for (int k = t * PPS; k < (t + 1) * PPS && k < PIECES; ++k) halo_piece(cp + 1, buf ^ 1, k);
       }
       const AFrag& a = abuf[t % 3];
+#if M16R_FLAT
+      // B fragments one 16-px block ahead, across tap boundaries (the first block of tap t + 1 is
+      // read during the last block of tap t): the MFMA pipe never waits for a step's first B read
+#pragma unroll
+      for (int pb = 0; pb < NPX; ++pb) {
+        const int idx = t * NPX + pb, cur = idx & 1;
+        if (idx + 1 < 9 * NPX) {
+          const int t1 = (idx + 1) / NPX, pb1 = (idx + 1) % NPX;
+          const int o1 = (((t1 / 3) + pb1 / TCB) * PITCH + (t1 % 3) + (pb1 % TCB) * 16) * 16;
+          bh[cur ^ 1] = *(const bf16x8g*)(hb + o1);
+          bl[cur ^ 1] = *(const bf16x8g*)(hb + o1 + HPLANE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl[cur], acc[cb][pb], 0, 0, 0);
+          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh[cur], acc[cb][pb], 0, 0, 0);
+        }
+      }
+#else
       const int toff = ((t / 3) * PITCH + (t % 3)) * 16;
       bf16x8g bh[2], bl[2];
       bh[0] = *(const bf16x8g*)(hb + toff);
@@ -166,6 +196,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh[cur], acc[cb][pb], 0, 0, 0);
         }
       }
+#endif
     }
     if (next) {
       // this wave's pieces of the next pair were issued by tap 4; younger than them are only the
