@@ -295,8 +295,8 @@ static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const Spl
 }
 
 // Tiling + launch of conv_m16r_bf16x3 for a 3x3 split-format conv; *taken = 0 when the shape is
-// outside it (the caller falls back to conv_m16k / conv_big).  mode: OP_M16R (0 off, 1 auto: 256
-// channels per workgroup where Co is a multiple of 256, else 128; 4 / 8 force NW).
+// outside it (the caller falls back to conv_m16k / conv_big).  mode: OP_M16R (0 off, 1 default:
+// NW 4; 8: NW 8 where Co is a multiple of 256).
 int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool, hipStream_t st, int* taken) {
   *taken = 0;
   static const int mode = getenv("OP_M16R") ? atoi(getenv("OP_M16R")) : 1;
@@ -307,12 +307,10 @@ int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool
     cop_max = std::max(cop_max, g[i].cop);
   }
   if (pool && (s.groups != 1 || (s.h & 1) || (s.w & 1) || !s.relu)) return OP_OK;
-  int nw = (mode == 4 || mode == 8) ? mode : 4;
-  if (mode == 1) {
-    bool all256 = true;
-    for (int i = 0; i < s.groups; ++i) all256 = all256 && g[i].cop % 256 == 0;
-    nw = all256 ? 8 : 4;
-  }
+  // NW = 4 (128 channels, two workgroups per CU with independent per-pair barriers) by default: in
+  // an interleaved A/B it ran the 3x3 class 2 % faster than 256-channel workgroups on the
+  // 256/512-channel layers (profiles/r03/ab_r03a_m16r_nw.log); OP_M16R=8 selects those
+  const int nw = mode == 8 ? 8 : 4;
   if (nw == 8)
     for (int i = 0; i < s.groups; ++i)
       if (g[i].cop % 256) return OP_OK;
