@@ -107,6 +107,7 @@ struct SplitConvShape {
   int32_t n, h, w, pin, cs_in, pout, cs_out, c16, ks, relu, groups, cs_out32;
   int32_t halo_mode;  // 0 gather kernel; 7x7 only: 1 shared-weight halo (x1 buffer), 2 (x2 buffers); 3 co-split halo (all)
   int32_t splitk;     // 1: the 7x7 raster kernel may split input chunks over workgroups (small launches)
+  int32_t regw;       // 1: large launches may take the register-weight kernels (conv_m16r / conv_m16s)
 };
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st);
 // split-K workspace of a stream (conv_big.hip): floats a capture wanted but could not allocate,

@@ -300,7 +300,7 @@ static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const Spl
 int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool, hipStream_t st, int* taken) {
   *taken = 0;
   static const int mode = getenv("OP_M16R") ? atoi(getenv("OP_M16R")) : 1;
-  if (!mode || s.ks != 3 || s.pin < 1 || s.cs_in % 16 || (s.c16 & 1) || s.halo_mode != 4) return OP_OK;
+  if (!mode || s.ks != 3 || s.pin < 1 || s.cs_in % 16 || (s.c16 & 1) || s.halo_mode != 4 || !s.regw) return OP_OK;
   int cop_max = 0;
   for (int i = 0; i < s.groups; ++i) {
     if (g[i].cop % 128 || g[i].cin_off % 16) return OP_OK;

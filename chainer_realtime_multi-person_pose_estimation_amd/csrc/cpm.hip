@@ -281,6 +281,7 @@ SplitConvShape cshape(int n, const CAct& in, const CAct& out, int c16, int ks, b
   s.cs_out32 = 0;
   s.halo_mode = 4;
   s.splitk = splitk;
+  s.regw = 1;
   return s;
 }
 

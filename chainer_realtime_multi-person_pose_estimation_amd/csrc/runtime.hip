@@ -636,7 +636,8 @@ static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks
   s.relu = relu ? 1 : 0;
   s.groups = groups;
   s.cs_out32 = 0;
-  s.halo_mode = algo;
+  s.halo_mode = algo == 5 ? 4 : algo;  // 5: the default family without the register-weight kernels
+  s.regw = algo == 4 ? 1 : 0;
   s.splitk = splitk;
   return s;
 }
@@ -668,7 +669,7 @@ static int pool(op_ctx* c, const Act& in, const Act& out, int ch);
 // one fused launch on the split path with the conv_big families (the pooled tensor is the only
 // output), else the conv into `full` and the pool kernel.
 static int conv_pool(op_ctx* c, const Act& in, const Act& full, const Act& pooled, const PackedConv& pc, int ch) {
-  if (c->split && c->conv_algo == 4) {
+  if (c->split && (c->conv_algo == 4 || c->conv_algo == 5)) {
     SplitConvGroup g[2];
     g[0] = sgrp(in, 0, pooled, 0, pc, ch);
     g[1] = g[0];
@@ -790,7 +791,7 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   // conv1_1 + conv1_2 + pool in one launch (conv1_pair.hip); OP_CONV1_FUSED=0: the two-kernel path
   static const bool c1_fused = !(getenv("OP_CONV1_FUSED") && atoi(getenv("OP_CONV1_FUSED")) == 0);
   bool conv1_done = false;
-  if (c->split && c1_fused && !c11_mfma && c->conv_algo == 4) {
+  if (c->split && c1_fused && !c11_mfma && (c->conv_algo == 4 || c->conv_algo == 5)) {
     const Act& o = B[B_C11];
     double fl = 0, by = 0;
     conv_work(c, o, c->bb[0], &fl, &by);
@@ -1237,7 +1238,7 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
   for (int i = 0; i < 4; ++i) hipEventCreate(&c->ev[i]);
   if (const char* e = getenv("OP_HALO_MODE")) {
     const int m = atoi(e);
-    if (m == 0 || m == 3 || m == 4) op::g_halo_mode = m;
+    if (m == 0 || m == 3 || m == 4 || m == 5) op::g_halo_mode = m;
   }
   c->conv_algo = op::g_halo_mode;
   if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
@@ -2726,8 +2727,9 @@ int op_set_batch_invariant(op_ctx* c, int32_t enable) {
 int op_set_conv_algo(op_ctx* c, int32_t algo) {
   using namespace op;
   RC(check_ctx(c, false));
-  if (algo != 0 && algo != 3 && algo != 4) {
-    set_error("conv algo must be 0 (per-tap gather), 3 (co-split halo) or 4 (default)");
+  if (algo != 0 && algo != 3 && algo != 4 && algo != 5) {
+    set_error("conv algo must be 0 (per-tap gather), 3 (co-split halo), 4 (default) or 5 (default without the "
+              "register-weight kernels)");
     return OP_ERR_INVALID;
   }
   c->conv_algo = algo;
