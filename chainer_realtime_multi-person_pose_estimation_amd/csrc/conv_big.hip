@@ -804,10 +804,6 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   BigTiling tl{};
   if (s.ks == 7) {
     if (!c128) return OP_OK;
-    {  // large launches: the register-weight, double-buffered-halo kernel (same accumulation order)
-      const int rc = launch_conv_m16s(s, g, device_zeros(), st, taken);
-      if (rc != OP_OK || *taken) return rc;
-    }
     if (raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
       // Tile size per launch shape.  A workgroup's time grows as ~(2 + NPX) (fixed halo /

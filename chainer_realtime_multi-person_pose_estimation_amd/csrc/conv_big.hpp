@@ -90,9 +90,6 @@ int launch_m16k_wide(dim3 grid, int lds, hipStream_t st, const SplitConvShape& s
 // when the shape or launch size is outside it
 int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool, hipStream_t st, int* taken);
 
-// conv_m16s.hip: the register-weight, double-buffered-halo 7x7 kernel (large launches of 46-wide maps)
-int launch_conv_m16s(const SplitConvShape& s, const SplitConvGroup* g, const void* zeros, hipStream_t st, int* taken);
-
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl);
 

@@ -96,10 +96,10 @@ int op_set_precision(op_ctx* ctx, int32_t mode);
 int op_get_precision(op_ctx* ctx, int32_t* mode);
 
 /* Kernel family of the bf16x3 convolutions (a tuning knob; every family computes the same
- * products, parity-tested): 4 (default): large launches (>= 512 workgroups) take the
- * register-weight kernels with double-buffered halos -- conv_m16r (3x3) and conv_m16s (7x7 on
- * 46-wide maps), which sum in exactly the order of the kernels below, so results are bit-identical
- * to 5; 5 = 4 without them: shared-weight halo tiles (conv_big.hip): the 7x7 layers
+ * products, parity-tested): 4 (default): large 3x3 launches (>= 1024 workgroups) take the
+ * register-weight kernel with a double-buffered halo, conv_m16r, which sums in exactly the order of
+ * conv_m16k below, so results are bit-identical to 5; 5 = 4 without it: shared-weight halo tiles
+ * (conv_big.hip): the 7x7 layers
  * on v_mfma_f32_16x16x32_bf16 tap pairs over raster tiles (640-pixel ranges of the batch that
  * span frame borders), the 3x3 layers on 16x16x32 with K = 32 input channels over 8 x 32 / 4 x 48
  * tiles (32x32x16 kernel for the 64-channel ones), the 1x1 layers on co-split halo tiles;
@@ -280,7 +280,6 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_3X3_R256 19    /* conv_m16r_bf16x3<8, ...> (register weights, 256 channels per workgroup) */
 #define OP_CENSUS_3X3_R128 20    /* conv_m16r_bf16x3<4, ...> (128 channels per workgroup) */
 #define OP_CENSUS_3X3_R_POOL 21  /* conv_m16r_bf16x3<., ., ., true> (fused 2x2 max-pool) */
-#define OP_CENSUS_7X7_S 22       /* conv_m16s_bf16x3 (register weights, double-buffered halo, 480-px tiles) */
 #define OP_CENSUS_SLOTS 24
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

@@ -53,10 +53,10 @@ def _max_err(a, b):
 
 @pytest.mark.parametrize("n,npx", [(38, 10), (57, 8), (114, 10)])
 def test_forward_at_bench_batches_vs_fixture_and_single_frames(lib, bctx, n, npx):
-    """Both kernel sets at the bench's batches: conv algo 5 (the round-2 kernels: conv_m16 raster
-    tap pairs with NPX-block tiles, conv_m16k) and the default 4 (large launches on the
-    register-weight kernels conv_m16s / conv_m16r).  Every frame of both == that frame alone, bit
-    for bit; the fixture frames <= 1e-3 from the reference network's own output."""
+    """Both kernel sets at the bench's batches: conv algo 5 (conv_m16 raster tap pairs with NPX-block
+    tiles, conv_m16k) and the default 4 (large 3x3 launches on the register-weight kernel
+    conv_m16r).  Every frame of both == that frame alone, bit for bit; the fixture frames <= 1e-3
+    from the reference network's own output."""
     _, d = load_case("posenet_1x368x368")
     xf = d["x"][0]
     rng = np.random.default_rng(n)
@@ -76,7 +76,7 @@ def test_forward_at_bench_batches_vs_fixture_and_single_frames(lib, bctx, n, npx
             bctx.set_conv_algo(4)
         # every 7x7 launch of this batch ran the NPX instantiation the cost model picks for it
         assert set(cen["npx"]) == {npx}, cen
-        assert cen["npx"][npx] == 5 * 5 and cen["7x7_splitk"] == 0 and cen["7x7_s"] == 0, cen  # 5 stages x Mconv1..5
+        assert cen["npx"][npx] == 5 * 5 and cen["7x7_splitk"] == 0, cen  # 5 stages x Mconv1..5
         for i in fixture_at:
             e = max(_max_err(paf[i], d["paf"][0]), _max_err(heat[i], d["heat"][0]))
             print("batch %d frame %d vs reference fixture: %.3g" % (n, i, e))
@@ -84,14 +84,14 @@ def test_forward_at_bench_batches_vs_fixture_and_single_frames(lib, bctx, n, npx
         # frames holding the same input agree bit for bit wherever they sit in the batch
         for i in fixture_at[1:]:
             assert np.array_equal(paf[i], paf[0]) and np.array_equal(heat[i], heat[0]), i
-        # the default kernels (register-weight 7x7 and 3x3 on the large launches): the same bits
+        # the default kernels (the register-weight 3x3 on the large launches): the same bits
         _census_npx(lib)
         paf4, heat4 = bctx.forward(x)
         cen4 = _census_npx(lib)
         print("batch %d default kernels:" % n, cen4)
-        assert cen4["7x7_s"] + sum(cen4["npx"].values()) == 25, cen4
-        if n >= 57:  # >= 512 workgroups per 7x7 launch
-            assert cen4["7x7_s"] == 25 and cen4["3x3_r128"] + cen4["3x3_r_pool"] >= 8, cen4
+        assert cen4["npx"] == {npx: 25}, cen4
+        if n >= 57:
+            assert cen4["3x3_r128"] + cen4["3x3_r_pool"] >= 8, cen4
         assert np.array_equal(paf4, paf) and np.array_equal(heat4, heat)
         # every frame == the same frame run alone (NPX 2 tiles, one frame per launch)
         for i in range(n):
@@ -126,7 +126,7 @@ def test_staged_u8_path_at_the_headline_batch(lib, bctx):
             paf, heat = bctx.fetch_maps(0, n)
         finally:
             pinned.close()
-        assert cen["7x7_s"] == 25 and not cen["npx"], cen  # the register-weight 7x7 kernel
+        assert set(cen["npx"]) == {10} and cen["npx"][10] == 25, cen
         assert cen["conv1_pair"] == 1 and cen["3x3_splitk"] == 0, cen
         # the register-weight 3x3 kernel runs the large 3x3 launches of this batch (bit-identical to
         # conv_m16k, which the single-frame runs below take: asserted by the per-frame comparison)

@@ -32,7 +32,10 @@ def pmc(d, sub, counter):
 
 
 # FETCH_SIZE -> bytes, by kernel (dominant read pattern); default: the guide's 16-B/lane stream
-FETCH_FACTOR = (("conv_m16_bf16x3", 536870912 / 545724096), ("conv_m16k_bf16x3", 268435456 / 240281984))
+# (round 3: conv_m16s loads its halo in the 7x7 pattern, conv_m16r in the 3x3 chunk-pair pattern;
+# their register weight fragments are L2 hits after the first workgroup and barely reach FETCH_SIZE)
+FETCH_FACTOR = (("conv_m16_bf16x3", 536870912 / 545724096), ("conv_m16s_bf16x3", 536870912 / 545724096),
+                ("conv_m16k_bf16x3", 268435456 / 240281984), ("conv_m16r_bf16x3", 268435456 / 240281984))
 
 
 def fetch_factor(name):
