@@ -32,9 +32,12 @@ constexpr int kP1Slots = kP1HR * kP1HC;            // 340
 // bytes per plane, a multiple of 256 so all 8 planes start on bank 0: a ds_read_b128 lane group
 // spans two planes (k-halves), and with a 64-B plane offset their 16-B slots collided (2-way)
 constexpr int kP1Plane = (kP1Slots * 16 + 255) / 256 * 256;  // (no measurable change in an A/B)
-constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
+[[maybe_unused]] constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
 #ifndef C1P_COW
 #define C1P_COW 32
+#endif
+#ifndef C1P_MFMA11
+#define C1P_MFMA11 1  // conv1_1 on MFMA (0: the f32 VALU form, in the CPU oracle's FMA order)
 #endif
 constexpr int kP1CoW = C1P_COW;             // conv1_2 output channels per wave (16, 32 or 64)
 constexpr int kP1Ncb = kP1CoW / 16;         // 16-channel MFMA blocks per wave
@@ -120,6 +123,69 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
   load_a(0, 0, ah, al);
   for (int half = 0; half < 2; ++half) {
     __syncthreads();  // input window staged / the previous half's MFMAs are done with the halo
+#if C1P_MFMA11
+    // ---- conv1_1 for channels 32*half .. +31 on the 10 x 34 window -> split LDS planes, on MFMA:
+    // K = the 27 (tap, input channel) products + 5 zeros, im2col fragments built in registers from
+    // the staged window, three bf16 products per MAC like every other layer (round 3: the f32 VALU
+    // form below took ~75 % of the workgroup's MFMA time in issue slots) ----
+    {
+      bf16x8p a11h[2], a11l[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int co = 32 * half + 16 * cb + l16;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * kg + j;
+          const float v = k < 27 ? wt11[k * 64 + co] : 0.0f;
+          const __bf16 h = (__bf16)v;
+          a11h[cb][j] = h;
+          a11l[cb][j] = (__bf16)(v - (float)h);
+        }
+      }
+      for (int blk = wave; blk < (kP1Slots + 15) / 16; blk += 4) {
+        const int sl = blk * 16 + l16;  // window slot = halo slot (row-major, pitch kP1HC)
+        const int ry = sl / kP1HC, rx = sl - (sl / kP1HC) * kP1HC;
+        bf16x8p bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * kg + j;
+          float v = 0.0f;
+          if (k < 27 && sl < kP1Slots) {
+            const int t = k / 3, ci = k - (k / 3) * 3;
+            v = inw[ci * kP1IR * kP1IC + (ry + t / 3) * kP1IC + rx + t % 3];
+          }
+          const __bf16 h = (__bf16)v;
+          bh[j] = h;
+          bl[j] = (__bf16)(v - (float)h);
+        }
+        const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
+        const bool inside = sl < kP1Slots && gy >= 0 && gy < h && gx >= 0 && gx < w;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          floatx4 d = {0.f, 0.f, 0.f, 0.f};
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11h[cb], bh, d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11h[cb], bl, d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11l[cb], bh, d, 0, 0, 0);
+          // lane: channels 16 cb + 4 kg .. + 3 of slot sl -> 8 bytes of the (chunk cb, half kg / 2)
+          // hi and lo planes (conv1_2's zero padding outside the image)
+          u16x4p hv, lv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float f = __fadd_rn(d[e], b11[32 * half + 16 * cb + 4 * kg + e]);
+            f = f > 0.0f && inside ? f : 0.0f;
+            const __bf16 hh = (__bf16)f;
+            hv[e] = __builtin_bit_cast(unsigned short, hh);
+            lv[e] = __builtin_bit_cast(unsigned short, (__bf16)(f - (float)hh));
+          }
+          if (sl < kP1Slots) {
+            char* dst = halo + (cb * 4 + 2 * (kg >> 1)) * kP1Plane + sl * 16 + (kg & 1) * 8;
+            *(u16x4p*)dst = hv;
+            *(u16x4p*)(dst + kP1Plane) = lv;
+          }
+        }
+      }
+    }
+#else
     // ---- conv1_1 for channels 32*half .. +31 on the 10 x 34 window -> split LDS planes ----
     for (int it = tid; it < 2 * kP1Items; it += 256) {
       // 16-channel group within the half: wave-uniform (kP1Items is a multiple of 64), so the
@@ -175,6 +241,7 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
         *(u16x8p*)(halo + (grp * 4 + 2 * k + 1) * kP1Plane + hs * 16) = lv[k];
       }
     }
+#endif
     __syncthreads();
     // ---- conv1_2, the 9 taps of this half: K = 32 channels per step ----
 #pragma unroll 1

@@ -23,11 +23,9 @@
 // CU; NW = 4: 128 channels, two per CU).  POOL: fused 2x2 max-pool epilogue (tile rows r, r + 1 =
 // blocks pb, pb + TCB; columns = lanes l, l ^ 1).  Layer semantics: models/CocoPoseNet.py:136-163
 // (conv + ReLU, the pools after conv1_2 / conv2_2 / conv3_4).
-#include "conv_big.hpp"
+#include <type_traits>
 
-#ifndef M16R_FLAT
-#define M16R_FLAT 1  // B fragments pipelined across tap boundaries (0: per tap, as conv_m16k)
-#endif
+#include "conv_big.hpp"
 
 namespace op {
 
@@ -38,10 +36,17 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory");
 }
 
-template <int NW, int TCB, int TR, bool POOL>
+template <int NW, int TCB, int TR, bool POOL, int CBW = 2>
 __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                    SplitConvGroup g1, BigTiling tl) {
-  constexpr int NPX = TR * TCB;           // 16-px blocks per wave (the whole pixel tile)
+  // CBW = 16-channel blocks per wave: 2 (waves split the channels only and cover the whole pixel
+  // tile) or 4 (NW = 4: two channel halves x two pixel halves -- every B fragment read from LDS
+  // feeds twice the MFMAs, every weight fragment is loaded by two waves)
+  static_assert(CBW == 2 || (CBW == 4 && NW == 4), "wave tiles: 32 channels, or 64 at NW 4");
+  constexpr int PGN = CBW / 2;              // pixel groups
+  constexpr int NCS = NW / PGN;             // channel slices
+  constexpr int NPT = TR * TCB;             // 16-px blocks of the tile
+  constexpr int NPX = NPT / PGN;            // 16-px blocks per wave
   constexpr int TC = 16 * TCB;
   constexpr int PITCH = TC + 2;
   constexpr int HROWS = TR + 2;
@@ -53,6 +58,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   constexpr int PPS = (PIECES + HSTEPS - 1) / HSTEPS;
   constexpr int CW = NW * 32;
   static_assert((8 * NH) % NW == 0, "halo pieces split evenly over the waves");
+  static_assert(NPT % PGN == 0 && (!POOL || (NPX % (2 * TCB)) == 0), "whole (pooled) row pairs per wave");
   static_assert(!POOL || (TR % 2 == 0), "pooled tiles hold whole row pairs");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [2][8 planes][NH KiB]
 
@@ -79,6 +85,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cs = wave % NCS, pg = wave / NCS;  // channel slice, pixel group
   const int l16 = lane & 15, kg = lane >> 4;
   const int csel = kg >> 1, khalf = kg & 1;
   const int wp_in = s.w + 2 * s.pin;
@@ -87,22 +94,24 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)lds;
 
-  // ---- A: this wave's 32 channels; weights [c16][tap][plane 2*khalf + hi/lo][cop][8 bf16] ----
+  // ---- A: this wave's 16*CBW channels; weights [c16][tap][plane 2*khalf + hi/lo][cop][8 bf16] ----
   const int64_t wplane = (int64_t)g.cop * 16;
-  const int cw0 = co0 + wave * 32;
+  const int cw0 = co0 + cs * 16 * CBW;
   const char* const wlane = (const char*)g.w + ((int64_t)csel * 9 * 4 + 2 * khalf) * wplane + (int64_t)(cw0 + l16) * 16;
   const int ncp = s.c16 / 2;
   const int n_it = ncp * 9;
-  typedef bf16x8g AFrag[4];  // [cb * 2 + hl]
-  AFrag abuf[3];
+  typedef bf16x8g AFrag[2 * CBW];  // [cb * 2 + hl]
+  constexpr int NB = CBW == 2 ? 3 : 2;  // weight buffers: 2 or 1 steps ahead (64-channel waves: registers)
+  AFrag abuf[NB];
   auto load_a = [&](int it, AFrag& a) {
     if (it >= n_it) it = n_it - 1;  // the last steps' prefetch re-reads the final step (unused)
     const int cp = it / 9, t = it - cp * 9;
     const char* p = wlane + (int64_t)((2 * cp * 9 + t) * 4) * wplane;
-    a[0] = *(const bf16x8g*)p;
-    a[1] = *(const bf16x8g*)(p + wplane);
-    a[2] = *(const bf16x8g*)(p + 256);
-    a[3] = *(const bf16x8g*)(p + wplane + 256);
+#pragma unroll
+    for (int cb = 0; cb < CBW; ++cb) {
+      a[2 * cb] = *(const bf16x8g*)(p + cb * 256);
+      a[2 * cb + 1] = *(const bf16x8g*)(p + wplane + cb * 256);
+    }
   };
 
   // ---- B: halo of one chunk pair; wave w DMAs pieces j = w, w + NW, ... (plane j / NH, piece j % NH) ----
@@ -120,44 +129,45 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   const int rows_here = min(TR, s.h - y0);
   const int cols_here = min(TC, s.w - x0);
   // this lane's halo byte offset within a buffer: plane of (chunk csel, half khalf, hi), pixel l16
-  const int bl0 = (csel * 4 + 2 * khalf) * HPLANE + l16 * 16;
+  // of the wave's first block (pixel group pg: tile rows pg * NPX / TCB ..)
+  const int bl0 = (csel * 4 + 2 * khalf) * HPLANE + (l16 + pg * (NPX / TCB) * PITCH) * 16;
 
-  floatx4 acc[2][NPX];
+  floatx4 acc[CBW][NPX];
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
+  for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk pair 0's halo into buffer 0, the first two steps' weights
+  // prologue: chunk pair 0's halo into buffer 0, the first NB - 1 steps' weights
 #pragma unroll
   for (int k = 0; k < PIECES; ++k) halo_piece(0, 0, k);
-  load_a(0, abuf[0]);
-  load_a(1, abuf[1]);
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k) load_a(k, abuf[k]);
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  for (int cp = 0; cp < ncp; ++cp) {
+  // one chunk pair (9 taps); P = the pair's parity, so step it = 9 cp + t uses weight buffer
+  // it % NB = (9 P + t) % NB at compile time (NB 3: t % 3; NB 2: the parity alternates per pair)
+  auto chunk_pair = [&](int cp, auto parity) {
+    constexpr int P = decltype(parity)::value;
     const int buf = cp & 1;
     const char* const hb = lds + buf * HBUF + bl0;
     const bool next = cp + 1 < ncp;
-#if M16R_FLAT
+    // B fragments one 16-px block ahead, across tap boundaries (the first block of tap t + 1 is
+    // read during the last block of tap t)
     bf16x8g bh[2], bl[2];
     bh[0] = *(const bf16x8g*)hb;
     bl[0] = *(const bf16x8g*)(hb + HPLANE);
-#endif
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int it = cp * 9 + t;
-      load_a(it + 2, abuf[(t + 2) % 3]);  // two steps ahead (it % 3 == t % 3: 9 taps per pair)
+      load_a(it + NB - 1, abuf[(9 * P + t + NB - 1) % NB]);  // NB - 1 steps ahead
       if (t < HSTEPS && next) {
 #pragma unroll
         for (int k = t * PPS; k < (t + 1) * PPS && k < PIECES; ++k) halo_piece(cp + 1, buf ^ 1, k);
       }
-      const AFrag& a = abuf[t % 3];
-#if M16R_FLAT
-      // B fragments one 16-px block ahead, across tap boundaries (the first block of tap t + 1 is
-      // read during the last block of tap t): the MFMA pipe never waits for a step's first B read
+      const AFrag& a = abuf[(9 * P + t) % NB];
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
         const int idx = t * NPX + pb, cur = idx & 1;
@@ -169,41 +179,27 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
+        for (int cb = 0; cb < CBW; ++cb) {
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl[cur], acc[cb][pb], 0, 0, 0);
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh[cur], acc[cb][pb], 0, 0, 0);
         }
       }
-#else
-      const int toff = ((t / 3) * PITCH + (t % 3)) * 16;
-      bf16x8g bh[2], bl[2];
-      bh[0] = *(const bf16x8g*)(hb + toff);
-      bl[0] = *(const bf16x8g*)(hb + toff + HPLANE);
-#pragma unroll
-      for (int pb = 0; pb < NPX; ++pb) {
-        const int cur = pb & 1;
-        if (pb + 1 < NPX) {
-          const int q1 = ((pb + 1) / TCB) * PITCH + ((pb + 1) % TCB) * 16;
-          bh[cur ^ 1] = *(const bf16x8g*)(hb + toff + q1 * 16);
-          bl[cur ^ 1] = *(const bf16x8g*)(hb + toff + q1 * 16 + HPLANE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh[cur], acc[cb][pb], 0, 0, 0);
-        }
-      }
-#endif
     }
     if (next) {
       // this wave's pieces of the next pair were issued by tap 4; younger than them are only the
-      // weight loads of taps 5..8 (4 each): waiting down to 8 outstanding covers every piece
+      // weight loads of taps 5..8 (2 CBW each): waiting down to 8 outstanding covers every piece
       wait_vmcnt<8>();
       __builtin_amdgcn_s_barrier();  // every wave's pieces landed; this pair's buffer is free
       asm volatile("" ::: "memory");
+    }
+  };
+  if constexpr (NB == 3) {
+    for (int cp = 0; cp < ncp; ++cp) chunk_pair(cp, std::integral_constant<int, 0>());
+  } else {
+    for (int cp = 0; cp < ncp; cp += 2) {
+      chunk_pair(cp, std::integral_constant<int, 0>());
+      if (cp + 1 < ncp) chunk_pair(cp + 1, std::integral_constant<int, 1>());
     }
   }
   wait_vmcnt<0>();
@@ -214,13 +210,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
 #pragma unroll
     for (int pb = 0; pb < NPX; ++pb) {
       if ((pb / TCB) & 1) continue;  // odd tile rows are the pair partners
-      const int r = pb / TCB, c = (pb % TCB) * 16 + l16;
+      const int r = pg * (NPX / TCB) + pb / TCB, c = (pb % TCB) * 16 + l16;
       const int y = y0 + r, x = x0 + c;
       const bool store = r < rows_here && c < cols_here && (l16 & 1) == 0;
       char* optr = (char*)g.out +
                    ((int64_t)(frame * hp_out + y / 2 + s.pout) * wp_out + (x / 2 + s.pout)) * (int64_t)s.cs_out * 4;
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
+      for (int cb = 0; cb < CBW; ++cb) {
         const int co = cw0 + cb * 16 + 4 * kg;
         const bool live = co < g.cout_store;
         const floatx4 bv = live ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f};
@@ -256,13 +252,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   const int hp_out = s.h + 2 * s.pout;
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
-    const int r = pb / TCB, c = (pb % TCB) * 16 + l16;
+    const int r = pg * (NPX / TCB) + pb / TCB, c = (pb % TCB) * 16 + l16;
     const bool live = r < rows_here && c < cols_here;
     const int y = y0 + r, x = x0 + c;
     char* optr = (char*)g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
     float* o32 = g.out32 ? g.out32 + ((int64_t)(frame * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
+    for (int cb = 0; cb < CBW; ++cb) {
       const int co = cw0 + cb * 16 + 4 * kg;
       floatx4 v;
       uint32_t own[4], w[4];
@@ -275,7 +271,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   }
 }
 
-template <int NW, int TCB, int TR, bool POOL>
+template <int NW, int TCB, int TR, bool POOL, int CBW>
 static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const SplitConvGroup& g1, const BigTiling& tl,
                     hipStream_t st) {
   constexpr int PITCH = 16 * TCB + 2;
@@ -284,13 +280,13 @@ static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const Spl
   static_assert(LDS <= 160 * 1024 / (8 / NW), "workgroups per CU x LDS fits 160 KiB");
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16r_bf16x3<NW, TCB, TR, POOL>,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_m16r_bf16x3<NW, TCB, TR, POOL, CBW>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
     attr = true;
   }
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
                                  : (unsigned)(tl.units * tl.per_unit);
-  hipLaunchKernelGGL((conv_m16r_bf16x3<NW, TCB, TR, POOL>), dim3(blocks), dim3(NW * 64), LDS, st, s, g0, g1, tl);
+  hipLaunchKernelGGL((conv_m16r_bf16x3<NW, TCB, TR, POOL, CBW>), dim3(blocks), dim3(NW * 64), LDS, st, s, g0, g1, tl);
   return OP_OK;
 }
 
@@ -331,11 +327,15 @@ int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool
   *taken = 1;
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
   census_add(pool ? OP_CENSUS_3X3_R_POOL : nw == 8 ? OP_CENSUS_3X3_R256 : OP_CENSUS_3X3_R128);
+  // wave tile: 32 channels x the whole tile (CBW 2), or 64 channels x half the tile (CBW 4, NW 4)
+  static const int cbw = getenv("OP_M16R_CBW") ? atoi(getenv("OP_M16R_CBW")) : 2;
   int rc;
   if (nw == 8)
-    rc = pool ? launch_t<8, TCB, TR, true>(s, g[0], g1, t, st) : launch_t<8, TCB, TR, false>(s, g[0], g1, t, st);
+    rc = pool ? launch_t<8, TCB, TR, true, 2>(s, g[0], g1, t, st) : launch_t<8, TCB, TR, false, 2>(s, g[0], g1, t, st);
+  else if (cbw == 4)
+    rc = pool ? launch_t<4, TCB, TR, true, 4>(s, g[0], g1, t, st) : launch_t<4, TCB, TR, false, 4>(s, g[0], g1, t, st);
   else
-    rc = pool ? launch_t<4, TCB, TR, true>(s, g[0], g1, t, st) : launch_t<4, TCB, TR, false>(s, g[0], g1, t, st);
+    rc = pool ? launch_t<4, TCB, TR, true, 2>(s, g[0], g1, t, st) : launch_t<4, TCB, TR, false, 2>(s, g[0], g1, t, st);
   if (rc != OP_OK) return rc;
   OP_AFTER_LAUNCH("conv_m16r_bf16x3", st);
   OP_HIP_CHECK(hipGetLastError());
