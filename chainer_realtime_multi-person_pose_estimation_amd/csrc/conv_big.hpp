@@ -21,6 +21,8 @@ struct BigTiling {
   int32_t co_tiles;          // channel tiles per group
   int32_t per_unit;          // workgroups per weight set (= n * tiles_y * tiles_x)
   int32_t xpu;               // XCDs per weight set (8 / units), 0 = plain block order
+  int32_t pair;              // > 1 (conv_m16r): channel tiles of one group sharing an XCD set, a
+                             // pixel tile's tiles dispatched back to back (xpu = 8 * pair / units)
   int32_t hw, total;         // raster tiles: pixels per frame, pixels of the batch
   int32_t fa_tiles;          // > 0 (conv_m16): raster tiles aligned to frames, fa_tiles per frame
   int32_t per_xcd;           // > 0: pixel-major XCD order (conv_m16k): XCD x runs pixel tiles

@@ -137,7 +137,11 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(hc - R + s.pin, wp_in - 1);
+#ifdef M16_PLANAR_PROBE  // timing probe only (wrong maps): the access pattern of a [chunk][plane][y][x] layout
+        glds16((const void*)((in_a ? fbase : fbase_b) + ((int64_t)(c * 4 + h_plane) * hp_in * wp_in + yy * wp_in + xx) * 16), dst);
+#else
         glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
+#endif
         dst += 2 * 1024;
         hc += 2 * 64;
         while (hc >= tl.pitch) {

@@ -65,9 +65,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   const int lin = blockIdx.x;
   int unit, widx;
   if (tl.xpu) {
+    // XCD set su runs weight sets su*P .. su*P+P-1; consecutive slots of one XCD are one pixel
+    // tile's P channel tiles, so its input is read from HBM once per XCD set
     const int xcd = lin & 7, slot = lin >> 3;
-    unit = xcd / tl.xpu;
-    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
+    const int P = tl.pair > 1 ? tl.pair : 1;
+    const int su = xcd / tl.xpu, q = slot / P;
+    unit = su * P + (slot - q * P);
+    widx = q * tl.xpu + (xcd - su * tl.xpu);
   } else {
     unit = lin / tl.per_unit;
     widx = lin - unit * tl.per_unit;
@@ -284,7 +288,7 @@ static int launch_t(const SplitConvShape& s, const SplitConvGroup& g0, const Spl
                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
     attr = true;
   }
-  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu * std::max(tl.pair, 1))
                                  : (unsigned)(tl.units * tl.per_unit);
   hipLaunchKernelGGL((conv_m16r_bf16x3<NW, TCB, TR, POOL, CBW>), dim3(blocks), dim3(NW * 64), LDS, st, s, g0, g1, tl);
   return OP_OK;
@@ -320,7 +324,23 @@ int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool
   t.co_tiles = cop_max / (nw * 32);
   t.units = s.groups * t.co_tiles;
   t.per_unit = s.n * t.tiles_y * t.tiles_x;
-  t.xpu = (t.units <= 8 && 8 % t.units == 0) ? 8 / t.units : 0;
+  // channel tiles per XCD set: the most whose weights (split format, 4 B per weight) stay under
+  // OP_M16R_PAIR_KB (0 = one tile per set, the input read from HBM once per tile).  5000 KB (pairs
+  // for conv3_x / conv4_2 / conv4_3 / conv5_1, all four tiles of conv4_1): non-pooled reads 887 ->
+  // 632 MiB FETCH_SIZE per launch, pooled 1752 -> 1446, the 3x3 class 21.73 -> 21.53 ms per 114
+  // frames (profiles/r03/ab_r03d_*.log, fetch_r03d_*.txt); a 2600-KB cap pairs fewer layers and
+  // measured no gain
+  static const int pair_kb = getenv("OP_M16R_PAIR_KB") ? atoi(getenv("OP_M16R_PAIR_KB")) : 5000;
+  const int64_t tile_wbytes = (int64_t)nw * 32 * s.c16 * 16 * 9 * 4;
+  t.pair = 1;
+  for (int p = t.co_tiles; p > 1; --p)
+    if (t.co_tiles % p == 0 && p * tile_wbytes <= (int64_t)pair_kb * 1024 && (t.units / p) <= 8 &&
+        8 % (t.units / p) == 0) {
+      t.pair = p;
+      break;
+    }
+  t.xpu = (t.units / t.pair <= 8 && 8 % (t.units / t.pair) == 0) ? 8 * t.pair / t.units : 0;
+  if (!t.xpu) t.pair = 1;
   // enough workgroups to fill the chip several times; small launches keep conv_m16k (split-K)
   const int64_t wgs = (int64_t)t.units * t.per_unit;
   if (wgs < (nw == 8 ? 2 * 256 : 4 * 256)) return OP_OK;

@@ -340,6 +340,35 @@ def test_async_uploads_equal_staged_frames(ctx, lib, graph):
             p.close()
 
 
+def test_one_pinned_buffer_rewritten_after_upload_wait(ctx, lib):
+    """The op_upload_frames contract (include/openpose_hip.h): the host buffer may be rewritten
+    once op_upload_wait returns, even while the run consuming the copy is still in flight -- so a
+    caller can recycle ONE pinned buffer.  Each run still sees exactly its own frames."""
+    rng = np.random.default_rng(29)
+    batches = [rng.integers(0, 256, (2, 240, 320, 3), dtype=np.uint8) for _ in range(3)]
+    want = []
+    for b in batches:
+        ctx.stage_frames(b)
+        ctx.run_staged()
+        ctx.synchronize()
+        want.append(ctx.fetch_maps(0, len(b)))
+    pinned = lib.PinnedFrames(2, 240, 320)
+    try:
+        got = []
+        for b in batches:
+            pinned.array[...] = b
+            ctx.upload_frames(pinned.array)
+            ctx.run_staged()
+            ctx.upload_wait()
+            pinned.array[...] = 255 - b  # the run may still be executing; its copy has landed
+            ctx.synchronize()
+            got.append(ctx.fetch_maps(0, len(b)))
+        for k, (g, w) in enumerate(zip(got, want)):
+            assert np.array_equal(g[0], w[0]) and np.array_equal(g[1], w[1]), k
+    finally:
+        pinned.close()
+
+
 def test_staged_synthetic_maps_match_reference(ctx):
     d = load_golden("six_people")
     maps = np.concatenate([d["paf_low"], d["heat_low"]])[None].repeat(2, axis=0)
