@@ -108,7 +108,17 @@ struct SplitConvShape {
   int32_t halo_mode;  // 0 gather kernel; 7x7 only: 1 shared-weight halo (x1 buffer), 2 (x2 buffers); 3 co-split halo (all)
   int32_t splitk;     // 1: the 7x7 raster kernel may split input chunks over workgroups (small launches)
   int32_t regw;       // 1: large launches may take the register-weight kernels (conv_m16r / conv_m16s)
+  // 1: the input / output tensor is chunk-planar (only conv_m16_bf16x3 and its split-K reduce take
+  // it): per frame [16-channel chunk][4 planes: hi 0-7, lo 0-7, hi 8-15, lo 8-15][hp][wp][16 B]
+  // instead of [hp][wp][channels], same frame size, so a chunk's halo rows are contiguous runs
+  int32_t in_planar = 0, out_planar = 0;
 };
+// Bytes between a split tensor's consecutive 16-B channel pieces / consecutive pixels of a row, for
+// its layout (planar: [chunk][plane][hp][wp][16 B] per frame; else [hp][wp][cs])
+__host__ __device__ __forceinline__ int64_t split_piece_stride(int planar, int hp, int wp) {
+  return planar ? (int64_t)hp * wp * 16 : 16;
+}
+__host__ __device__ __forceinline__ int64_t split_pixel_stride(int planar, int cs) { return planar ? 16 : (int64_t)cs * 4; }
 int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st);
 // split-K workspace of a stream (conv_big.hip): floats a capture wanted but could not allocate,
 // grow to that size (outside capture; 0 ok), free on stream destruction
@@ -124,6 +134,7 @@ int launch_conv_halo(const SplitConvShape& s, const SplitConvGroup* g, hipStream
 // big-tile 7x7 kernel (conv_big.hip): one workgroup per CU, 128 channels x <= 768 pixels
 int conv_big_device_init(int device);  // per-device constants; call once per context, outside capture
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken);
+bool conv_m16_takes(int n, int h, int w, int groups, int cop_max);
 // process-wide launch census of the bf16x3 conv kernels by instantiation (op_conv_census; slots in
 // include/openpose_hip.h): incremented on the host at every launch (a graph replay adds nothing)
 void census_add(int slot);
@@ -145,6 +156,7 @@ struct HeadGroup {
 };
 struct HeadShape {
   int32_t n, h, w, pin, cs_in, pout, cs_out, ci, co1, groups, cs_out32;
+  int32_t in_planar = 0;  // 1: chunk-planar input (SplitConvShape::in_planar)
 };
 int launch_conv_head(const HeadShape& s, const HeadGroup* g, hipStream_t st, int* taken);
 int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,

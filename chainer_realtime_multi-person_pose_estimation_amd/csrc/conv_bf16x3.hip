@@ -219,6 +219,14 @@ int launch_conv_bf16x3(const SplitConvShape& s, const SplitConvGroup* g, hipStre
     }
     if (g[i].cop % 128) wide = false;
   }
+  // chunk-planar tensors (the stage buffers of stages 2-6): conv_m16_bf16x3 only
+  if (s.in_planar || s.out_planar) {
+    int taken = 0;
+    const int rc = s.ks == 7 && s.halo_mode == 4 ? launch_conv_big(s, g, st, &taken) : OP_OK;
+    if (rc || taken) return rc;
+    set_error("launch_conv_bf16x3: chunk-planar tensors need the conv_m16 7x7 kernel");
+    return OP_ERR_INVALID;
+  }
   // conv algo 4 (default): the shared-weight halo kernels (conv_big.hip), then the co-split halo
   // kernel for the shapes they leave (the 1x1 convs, narrow maps); algo 3: the co-split halo
   // kernel first; algo 0 / anything neither takes: the per-tap gather kernel below

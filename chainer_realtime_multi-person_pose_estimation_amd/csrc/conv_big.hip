@@ -488,9 +488,11 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
   }
   const int f = P / tl.hw, pp = P - f * tl.hw;
   const int y = pp / s.w, x = pp - y * s.w;
-  const int wp_out = s.w + 2 * s.pout;
-  char* d = (char*)g.out + ((int64_t)(f * (s.h + 2 * s.pout) + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4 +
-            (co >> 3) * 32 + (co & 7) * 2;
+  const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
+  const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
+  char* d = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
+            ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * split_pixel_stride(s.out_planar, s.cs_out) +
+            (co >> 3) * 2 * out_pc + (co & 7) * 2;
   u16x4g vh, vl;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
     vl[e] = __builtin_bit_cast(unsigned short, l16v);
   }
   *(u16x4g*)d = vh;
-  *(u16x4g*)(d + 16) = vl;
+  *(u16x4g*)(d + out_pc) = vl;
   if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
 }
 
@@ -790,6 +792,13 @@ int launch_conv_big_pool(const SplitConvShape& s, const SplitConvGroup* g, hipSt
 
 // The split-path convolution on shared-weight halo tiles (7x7 and 3x3).  *taken = 0 when the
 // shape is outside these kernels (the caller falls back).
+// whether launch_conv_big runs a 7x7 launch of this shape on conv_m16_bf16x3 (the only kernel
+// that reads and writes chunk-planar tensors)
+bool conv_m16_takes(int n, int h, int w, int groups, int cop_max) {
+  BigTiling tl{};
+  return cop_max % 128 == 0 && raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, n, h, w, groups, cop_max, tl, true);
+}
+
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
   *taken = 0;
   if ((s.ks != 7 && s.ks != 3) || s.cs_in % 16 || s.pin < s.ks / 2) return OP_OK;
@@ -895,6 +904,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       OP_HIP_CHECK(hipGetLastError());
       return OP_OK;
     }
+    if (s.in_planar || s.out_planar) return OP_OK;  // the caller reports it
     if (raster_tiling(BigConfig{7, 6, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl)) {
       if (plain_order) tl.xpu = 0;
       *taken = 1;

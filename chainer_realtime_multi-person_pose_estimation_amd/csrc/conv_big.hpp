@@ -70,17 +70,20 @@ __device__ __forceinline__ void split_pair_swap(const floatx4& acc, const floatx
 }
 
 // Store one lane's part of an 8-channel group (see split_pair_swap): one 16-B store when the whole
-// group is stored, else (a group cut by cout_store) this lane's own two 8-B pieces.
+// group is stored, else (a group cut by cout_store) this lane's own two 8-B pieces.  pstride = bytes
+// between the pixel's consecutive 16-B pieces: 16 in the [pixel][channels] layout, the plane size in
+// the chunk-planar one (SplitConvShape::out_planar).
 __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, int cout_store, const uint32_t own[4],
-                                                  const uint32_t w[4]) {
-  char* gp = optr + (co >> 3) * 32;
+                                                  const uint32_t w[4], int64_t pstride = 16) {
+  char* gp = optr + (co >> 3) * 2 * pstride;
   if ((co | 7) < cout_store) {
-    *(uint4*)(gp + (kg & 1) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)(gp + (kg & 1) * pstride) = make_uint4(w[0], w[1], w[2], w[3]);
   } else {
     *(uint2*)(gp + (co & 7) * 2) = make_uint2(own[0], own[1]);
-    *(uint2*)(gp + 16 + (co & 7) * 2) = make_uint2(own[2], own[3]);
+    *(uint2*)(gp + pstride + (co & 7) * 2) = make_uint2(own[2], own[3]);
   }
 }
+
 
 // conv_m16.hip: launch conv_m16_bf16x3<7, npx, deep> on a raster tiling made by conv_big.hip (picks
 // the deep weight ring for small tiles; sets the kernels' LDS attribute on first use).

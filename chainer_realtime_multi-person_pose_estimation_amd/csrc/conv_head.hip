@@ -73,13 +73,18 @@ __global__ __launch_bounds__(256, ONE ? 4 : 2) void conv_head_bf16x3(HeadShape s
   load_a1(0);
   // ---- input tile -> LDS (16-B pieces; pixels past the batch repeat the last one) ----
   {
+    // (chunk-planar input: consecutive threads take consecutive pixels of one plane, so a wave
+    // reads 64 contiguous 16-B pieces; else one pixel's consecutive pieces)
     constexpr int pieces = CI / 4;
+    const int64_t pcs = split_piece_stride(s.in_planar, hp_in, wp_in), pxs = split_pixel_stride(s.in_planar, s.cs_in);
     for (int i = threadIdx.x; i < kHeadPx * pieces; i += 256) {
-      const int px = i / pieces, pc = i - px * pieces;
+      const int px = s.in_planar ? i % kHeadPx : i / pieces;
+      const int pc = s.in_planar ? i / kHeadPx : i - px * pieces;
       const int P = min(P0 + px, total - 1);
       const int f = P / hw, pp = P - f * hw;
       const int y = pp / s.w, x = pp - y * s.w;
-      const float* src = g.in + ((int64_t)(f * hp_in + y + s.pin) * wp_in + x + s.pin) * s.cs_in + pc * 4;
+      const char* src = (const char*)g.in + (int64_t)f * hp_in * wp_in * s.cs_in * 4 +
+                        ((int64_t)(y + s.pin) * wp_in + x + s.pin) * pxs + pc * pcs;
       *(uint4*)(X + px * xpitch + pc * 16) = *(const uint4*)src;
     }
   }

@@ -74,6 +74,10 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int64_t pix_bytes = (int64_t)s.cs_in * 4;
   const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
   const char* const fbase_b = (const char*)g.in + (int64_t)fb * hp_in * wp_in * pix_bytes;
+  // a chunk's 4 halo planes: 16-B pieces of each pixel record, or (chunk-planar input) 4 planes of
+  // contiguous rows, so each wave's 64 x 16 B read is one 1-KiB run
+  const int64_t in_pc = split_piece_stride(s.in_planar, hp_in, wp_in);
+  const int64_t in_px = split_pixel_stride(s.in_planar, s.cs_in);
 
   // weights: wave w copies piece w: plane w / 2, channels co0 + 64*(w % 2) + 0..63
   const int64_t wplane = (int64_t)g.cop * 16;
@@ -129,19 +133,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     {
-      const char* src0 = fbase + c * 64 + h_plane * 16;
-      const char* src0_b = fbase_b + c * 64 + h_plane * 16;
+      const char* src0 = fbase + (int64_t)(c * 4 + h_plane) * in_pc;
+      const char* src0_b = fbase_b + (int64_t)(c * 4 + h_plane) * in_pc;
       int hr = h_r0, hc = h_c0;
       char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
       for (int i = h_i0; i < tl.nh; i += 2) {
         const bool in_a = hr < rowsA;
         const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
         const int xx = min(hc - R + s.pin, wp_in - 1);
-#ifdef M16_PLANAR_PROBE  // timing probe only (wrong maps): the access pattern of a [chunk][plane][y][x] layout
-        glds16((const void*)((in_a ? fbase : fbase_b) + ((int64_t)(c * 4 + h_plane) * hp_in * wp_in + yy * wp_in + xx) * 16), dst);
-#else
-        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * pix_bytes), dst);
-#endif
+        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * in_px), dst);
         dst += 2 * 1024;
         hc += 2 * 64;
         while (hc >= tl.pitch) {
@@ -213,12 +213,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
+  const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
+  const int64_t out_px = split_pixel_stride(s.out_planar, s.cs_out);
 #pragma unroll
   for (int pb = 0; pb < NPX; ++pb) {
     const int P = P0 + (pg * NPX + pb) * 16 + l16;
     const int f = P / tl.hw, pp = P - f * tl.hw;
     const int y = pp / s.w, x = pp - y * s.w;
-    char* optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + (x + s.pout)) * (int64_t)s.cs_out * 4;
+    char* optr = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
+                 ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * out_px;
     float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
                       v, own, w);
       if (P > P1 || co >= g.cout_store) continue;
-      store_split_group(optr, co, kg, g.cout_store, own, w);
+      store_split_group(optr, co, kg, g.cout_store, own, w, out_pc);
       if (o32) *(floatx4*)(o32 + co) = v;
     }
   }

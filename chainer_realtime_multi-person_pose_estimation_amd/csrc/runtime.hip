@@ -212,6 +212,7 @@ static int round_up(int v, int m) { return (v + m - 1) / m * m; }
 struct Act {
   float* p = nullptr;
   int pad = 0, cs = 0, h = 0, w = 0;
+  int planar = 0;  // split layout: 0 [frame][hp][wp][cs], 1 chunk-planar (SplitConvShape::in_planar)
   size_t frame_floats() const { return (size_t)(h + 2 * pad) * (w + 2 * pad) * cs; }
 };
 
@@ -246,7 +247,7 @@ struct KeepSlot {
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
-  B_S1, B_MAP32, B_COUNT
+  B_S1, B_MAP32, B_PA, B_PB, B_COUNT
 };
 
 }  // namespace op
@@ -367,7 +368,7 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
   const D d[B_COUNT] = {{1, 8, 1},   {1, 64, 1},  {0, 64, 1},  {1, 64, 2},  {1, 128, 2}, {0, 128, 2},
                         {1, 128, 4}, {1, 256, 4}, {1, 256, 4}, {0, 256, 4}, {1, 256, 8}, {1, 512, 8},
                         {1, 512, 8}, {1, 256, 8}, {kStagePad, kCatStride, 8}, {kStagePad, 256, 8},
-                        {kStagePad, 256, 8}, {0, 1024, 8}, {0, 64, 8}};
+                        {kStagePad, 256, 8}, {0, 1024, 8}, {0, 64, 8}, {kStagePad, 256, 8}, {kStagePad, 256, 8}};
   size_t total = 0;
   for (int i = 0; i < B_COUNT; ++i) {
     Act a;
@@ -375,6 +376,7 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
     a.cs = (i == B_X0 && split) ? 16 : d[i].cs;
     a.h = h / d[i].div;
     a.w = w / d[i].div;
+    a.planar = (i == B_PA || i == B_PB) ? 1 : 0;  // the 7x7 stage buffers of stages 2-6
     const size_t fl = a.frame_floats() * (size_t)n;
     if (out) {
       out[i] = a;
@@ -387,7 +389,8 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
 }
 
 static const char* const kBufName[B_COUNT] = {"X0",  "C11", "C12", "P1",  "C21", "C22", "P2",  "C3A", "C3B", "C34",
-                                              "P3",  "C41", "C42", "C43", "CAT", "BRA", "BRB", "S1",  "MAP32"};
+                                              "P3",  "C41", "C42", "C43", "CAT", "BRA", "BRB", "S1",  "MAP32",
+                                              "PA",  "PB"};
 
 static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   if (h % 8 || w % 8 || h < 16 || w < 16 || n < 1) {
@@ -603,11 +606,16 @@ static void conv_work(const op_ctx* c, const Act& out, const PackedConv& pc, dou
   *bytes += 4.0 * (px * pc.cin_log + px * pc.co_log + (double)pc.cin_log * pc.co_log * pc.ks * pc.ks + pc.co_log);
 }
 
+// first channel `off` (a multiple of 8) of a split tensor, in floats from its base, for its layout
+static size_t chan_offset(const Act& a, int off) {
+  return a.planar ? (size_t)off * (a.h + 2 * a.pad) * (a.w + 2 * a.pad) : (size_t)off;
+}
+
 static SplitConvGroup sgrp(const Act& in, int cin_off, const Act& out, int cout_off, const PackedConv& pc,
                           int cout_store) {
   SplitConvGroup g;
-  g.in = in.p + cin_off;
-  g.out = out.p + cout_off;
+  g.in = in.p + chan_offset(in, cin_off);
+  g.out = out.p + chan_offset(out, cout_off);
   g.w = pc.ws;
   g.bias = pc.b;
   g.cop = pc.cop;
@@ -639,6 +647,8 @@ static SplitConvShape sshp(int n, const Act& in, const Act& out, int c16, int ks
   s.halo_mode = algo == 5 ? 4 : algo;  // 5: the default family without the register-weight kernels
   s.regw = algo == 4 ? 1 : 0;
   s.splitk = splitk;
+  s.in_planar = in.planar;
+  s.out_planar = out.planar;
   return s;
 }
 
@@ -726,10 +736,14 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
 // Fused 1x1 pair per branch (conv5_4+conv5_5, Mconv6+Mconv7): in -> a (ReLU) -> b -> out, the
 // intermediate kept on chip (conv_head.hip).  Returns -1 when not taken (the caller then runs the
 // two convs through `mid`).  OP_HEAD_FUSED=0 disables it (A/B).
+static bool head_fused_on() {
+  static const bool off = getenv("OP_HEAD_FUSED") && atoi(getenv("OP_HEAD_FUSED")) == 0;
+  return !off;
+}
+
 static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1,
                  const PackedConv* a, const PackedConv* b, int st0, int st1, const Act* out32, int o32a, int o32b) {
-  static const bool off = getenv("OP_HEAD_FUSED") && atoi(getenv("OP_HEAD_FUSED")) == 0;
-  if (!c->split || off) return -1;
+  if (!c->split || !head_fused_on()) return -1;
   HeadShape s;
   s.n = c->gn;
   s.h = out.h;
@@ -742,10 +756,11 @@ static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
   s.co1 = a[0].cop;
   s.groups = 2;
   s.cs_out32 = out32 ? out32->cs : 0;
+  s.in_planar = in.planar;
   HeadGroup g[2];
   const int cis[2] = {ci0, ci1}, cos[2] = {co0, co1}, sts[2] = {st0, st1}, o32[2] = {o32a, o32b};
   for (int i = 0; i < 2; ++i) {
-    g[i].in = in.p + cis[i];
+    g[i].in = in.p + chan_offset(in, cis[i]);
     g[i].w1 = a[i].ws;
     g[i].b1 = a[i].b;
     g[i].cop1 = a[i].cop;
@@ -840,13 +855,21 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
     }
     RC(dump_stage(0));
   }
-  // stages 2-6 (CocoPoseNet.py:167-260)
+  // stages 2-6 (CocoPoseNet.py:167-260).  Mconv1..Mconv5 outputs go to the chunk-planar stage
+  // buffers when conv_m16_bf16x3 takes every 7x7 launch of this geometry and the fused head reads
+  // Mconv5's output (OP_STAGE_PLANAR=0: the [pixel][channels] buffers, A/B aid)
   Act s6 = B[B_S1];
   s6.cs = 256;  // Mconv6 output reuses the stage-1 1x1 buffer (no halo) with a 256-channel stride
+  static const bool planar_env = !(getenv("OP_STAGE_PLANAR") && atoi(getenv("OP_STAGE_PLANAR")) == 0);
+  const int sh8 = B[B_BRA].h, sw8 = B[B_BRA].w;
+  const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && planar_env && head_fused_on() &&
+                      conv_m16_takes(c->gn, sh8, sw8, 1, 256) && conv_m16_takes(c->gn, sh8, sw8, 2, 128);
+  const Act& SA = planar ? B[B_PA] : B[B_BRA];
+  const Act& SB = planar ? B[B_PB] : B[B_BRB];
   for (int st = 0; st < 5; ++st) {
-    RC(conv1(c, cat, 0, B[B_BRA], 0, c->st_first[st], 256, true));
-    const Act* src = &B[B_BRA];
-    const Act* dst = &B[B_BRB];
+    RC(conv1(c, cat, 0, SA, 0, c->st_first[st], 256, true));
+    const Act* src = &SA;
+    const Act* dst = &SB;
     c->prof_join = true;  // Mconv2..Mconv5 follow Mconv1 back to back on the stream
     for (int i = 0; i < 4; ++i) {
       const int r = conv2(c, *src, 0, 128, *dst, 0, 128, c->st_g[st][0][i], c->st_g[st][1][i], 128, 128, true);
