@@ -156,12 +156,16 @@ struct HeadGroup {
 };
 struct HeadShape {
   int32_t n, h, w, pin, cs_in, pout, cs_out, ci, co1, groups, cs_out32;
-  int32_t in_planar = 0;  // 1: chunk-planar input (SplitConvShape::in_planar)
+  int32_t in_planar = 0, out_planar = 0;  // 1: chunk-planar input / output (SplitConvShape::in_planar)
 };
 int launch_conv_head(const HeadShape& s, const HeadGroup* g, hipStream_t st, int* taken);
 int launch_maxpool2_split(const float* in, int32_t pin, float* out, int32_t pout, int32_t n, int32_t h, int32_t w,
                           int32_t c, hipStream_t st);
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st);
+// the first c16 16-channel chunks of every interior pixel of a split [pixel][channels] tensor ->
+// the same channels of a chunk-planar tensor of the same geometry (pad, channel stride cs)
+int launch_split_to_planar(const float* in, float* out, int32_t n, int32_t h, int32_t w, int32_t pad, int32_t cs,
+                           int32_t c16, hipStream_t st);
 int launch_preprocess_split(const uint8_t* frames, int64_t frame_bytes, int64_t row_stride, int32_t n, int32_t sh,
                             int32_t sw, int32_t dh, int32_t dw, float* out, hipStream_t st, float div = 255.0f);
 int launch_extract_maps32(const float* m, int32_t cs, int32_t heat_off, int32_t n, int32_t h, int32_t w, float* paf,

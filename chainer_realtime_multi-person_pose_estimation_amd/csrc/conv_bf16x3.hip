@@ -358,6 +358,38 @@ __global__ __launch_bounds__(256) void nchw_to_split16(const float* __restrict__
   store_split8(out + i * 64 + 32, z);
 }
 
+// 16-B piece i of pixel p (32 threads per pixel of a 128-channel slice: the reads are one
+// contiguous run per pixel; the writes land in 4 * c16 planes, merged into lines in L2)
+__global__ __launch_bounds__(256) void split_to_planar(const char* __restrict__ in, char* __restrict__ out, int32_t n,
+                                                       int32_t h, int32_t w, int32_t pad, int32_t cs, int32_t c16) {
+  const int pieces = 4 * c16;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)n * h * w * pieces) return;
+  const int pc = (int)(i % pieces);
+  const int64_t P = i / pieces;
+  const int hw = h * w;
+  const int f = (int)(P / hw), pp = (int)(P - (int64_t)f * hw);
+  const int y = pp / w, x = pp - (pp / w) * w;
+  const int hp = h + 2 * pad, wp = w + 2 * pad;
+  const int64_t fb = (int64_t)f * hp * wp * cs * 4, pix = (int64_t)(y + pad) * wp + x + pad;
+  const uint4 v = *(const uint4*)(in + fb + pix * cs * 4 + pc * 16);
+  *(uint4*)(out + fb + (int64_t)pc * hp * wp * 16 + pix * 16) = v;
+}
+
+int launch_split_to_planar(const float* in, float* out, int32_t n, int32_t h, int32_t w, int32_t pad, int32_t cs,
+                           int32_t c16, hipStream_t st) {
+  if (cs % 16 || c16 * 16 > cs || n < 1) {
+    set_error("split_to_planar: bad channel range");
+    return OP_ERR_INVALID;
+  }
+  const int64_t items = (int64_t)n * h * w * 4 * c16;
+  hipLaunchKernelGGL(split_to_planar, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, (const char*)in,
+                     (char*)out, n, h, w, pad, cs, c16);
+  OP_AFTER_LAUNCH("split_to_planar", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 int launch_nchw_to_split16(const float* x, float* out, int32_t n, int32_t h, int32_t w, hipStream_t st) {
   const int64_t total = (int64_t)n * (h + 2) * (w + 2);
   hipLaunchKernelGGL(nchw_to_split16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, (char*)out, n, h, w);

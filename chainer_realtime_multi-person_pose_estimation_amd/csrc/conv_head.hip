@@ -175,7 +175,9 @@ __global__ __launch_bounds__(256, ONE ? 4 : 2) void conv_head_bf16x3(HeadShape s
   const int f = P / hw, pp = P - f * hw;
   const int y = pp / s.w, x = pp - y * s.w;
   const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
-  char* const optr = (char*)g.out + ((int64_t)(f * hp_out + y + s.pout) * wp_out + x + s.pout) * (int64_t)s.cs_out * 4;
+  const int64_t opc = split_piece_stride(s.out_planar, hp_out, wp_out);
+  char* const optr = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
+                     ((int64_t)(y + s.pout) * wp_out + x + s.pout) * split_pixel_stride(s.out_planar, s.cs_out);
   float* const o32 = g.out32 ? g.out32 + (int64_t)P * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
   for (int j = 0; j < NB2; ++j) {
@@ -193,9 +195,9 @@ __global__ __launch_bounds__(256, ONE ? 4 : 2) void conv_head_bf16x3(HeadShape s
       vh[e] = __builtin_bit_cast(unsigned short, h16);
       vl[e] = __builtin_bit_cast(unsigned short, l16v);
     }
-    char* d = optr + (co >> 3) * 32 + (co & 7) * 2;
+    char* d = optr + (co >> 3) * 2 * opc + (co & 7) * 2;
     *(u16x4h*)d = vh;
-    *(u16x4h*)(d + 16) = vl;
+    *(u16x4h*)(d + opc) = vl;
     if (o32) *(floatx4*)(o32 + co) = v;
   }
 }

@@ -67,11 +67,14 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
   if (tl.xpu) {
     // XCD set su runs weight sets su*P .. su*P+P-1; consecutive slots of one XCD are one pixel
     // tile's P channel tiles, so its input is read from HBM once per XCD set
+    // (per_xcd > 0: XCD xo of the set runs the contiguous pixel tiles [xo * per_xcd, +per_xcd), so
+    // vertically adjacent tiles run on one XCD at about the same time and share their halo rows
+    // in its L2; else consecutive tiles go to consecutive XCDs of the set)
     const int xcd = lin & 7, slot = lin >> 3;
     const int P = tl.pair > 1 ? tl.pair : 1;
-    const int su = xcd / tl.xpu, q = slot / P;
+    const int su = xcd / tl.xpu, q = slot / P, xo = xcd - su * tl.xpu;
     unit = su * P + (slot - q * P);
-    widx = q * tl.xpu + (xcd - su * tl.xpu);
+    widx = tl.per_xcd > 0 ? xo * tl.per_xcd + q : q * tl.xpu + xo;
   } else {
     unit = lin / tl.per_unit;
     widx = lin - unit * tl.per_unit;
@@ -341,6 +344,11 @@ int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool
     }
   t.xpu = (t.units / t.pair <= 8 && 8 % (t.units / t.pair) == 0) ? 8 * t.pair / t.units : 0;
   if (!t.xpu) t.pair = 1;
+  // contiguous pixel tiles per XCD (default; OP_M16R_XMAJ=0: consecutive tiles on consecutive XCDs):
+  // 3x3 fabric reads 1325 -> 998 MB per non-pooled launch, 3035 -> 1980 pooled, the 3x3 class
+  // 21.13 -> 20.94 ms per 114 frames (profiles/r03/ab_r03i_*.log, tcc_r03i_*.txt)
+  static const int xmaj = getenv("OP_M16R_XMAJ") ? atoi(getenv("OP_M16R_XMAJ")) : 1;
+  t.per_xcd = xmaj && t.xpu ? (t.per_unit + t.xpu - 1) / t.xpu : 0;
   // enough workgroups to fill the chip several times; small launches keep conv_m16k (split-K)
   const int64_t wgs = (int64_t)t.units * t.per_unit;
   if (wgs < (nw == 8 ? 2 * 256 : 4 * 256)) return OP_OK;

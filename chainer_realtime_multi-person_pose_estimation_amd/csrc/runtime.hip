@@ -247,7 +247,7 @@ struct KeepSlot {
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
-  B_S1, B_MAP32, B_PA, B_PB, B_COUNT
+  B_S1, B_MAP32, B_PA, B_PB, B_CATP, B_COUNT
 };
 
 }  // namespace op
@@ -368,7 +368,8 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
   const D d[B_COUNT] = {{1, 8, 1},   {1, 64, 1},  {0, 64, 1},  {1, 64, 2},  {1, 128, 2}, {0, 128, 2},
                         {1, 128, 4}, {1, 256, 4}, {1, 256, 4}, {0, 256, 4}, {1, 256, 8}, {1, 512, 8},
                         {1, 512, 8}, {1, 256, 8}, {kStagePad, kCatStride, 8}, {kStagePad, 256, 8},
-                        {kStagePad, 256, 8}, {0, 1024, 8}, {0, 64, 8}, {kStagePad, 256, 8}, {kStagePad, 256, 8}};
+                        {kStagePad, 256, 8}, {0, 1024, 8}, {0, 64, 8}, {kStagePad, 256, 8}, {kStagePad, 256, 8},
+                        {kStagePad, kCatStride, 8}};
   size_t total = 0;
   for (int i = 0; i < B_COUNT; ++i) {
     Act a;
@@ -376,7 +377,7 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
     a.cs = (i == B_X0 && split) ? 16 : d[i].cs;
     a.h = h / d[i].div;
     a.w = w / d[i].div;
-    a.planar = (i == B_PA || i == B_PB) ? 1 : 0;  // the 7x7 stage buffers of stages 2-6
+    a.planar = (i == B_PA || i == B_PB || i == B_CATP) ? 1 : 0;  // the 7x7 inputs of stages 2-6
     const size_t fl = a.frame_floats() * (size_t)n;
     if (out) {
       out[i] = a;
@@ -390,7 +391,7 @@ static size_t geom_floats(op_ctx* c, int n, int h, int w, Act* out, bool split) 
 
 static const char* const kBufName[B_COUNT] = {"X0",  "C11", "C12", "P1",  "C21", "C22", "P2",  "C3A", "C3B", "C34",
                                               "P3",  "C41", "C42", "C43", "CAT", "BRA", "BRB", "S1",  "MAP32",
-                                              "PA",  "PB"};
+                                              "PA",  "PB",  "CATP"};
 
 static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   if (h % 8 || w % 8 || h < 16 || w < 16 || n < 1) {
@@ -757,6 +758,7 @@ static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
   s.groups = 2;
   s.cs_out32 = out32 ? out32->cs : 0;
   s.in_planar = in.planar;
+  s.out_planar = out.planar;
   HeadGroup g[2];
   const int cis[2] = {ci0, ci1}, cos[2] = {co0, co1}, sts[2] = {st0, st1}, o32[2] = {o32a, o32b};
   for (int i = 0; i < 2; ++i) {
@@ -767,7 +769,7 @@ static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
     g[i].w2 = b[i].ws;
     g[i].b2 = b[i].b;
     g[i].cop2 = b[i].cop;
-    g[i].out = out.p + cos[i];
+    g[i].out = out.p + chan_offset(out, cos[i]);
     g[i].cout_store = sts[i];
     g[i].out32 = out32 ? out32->p : nullptr;
     g[i].out32_off = o32[i];
@@ -838,6 +840,19 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   RC(conv1(c, B[B_C41], 0, B[B_C42], 0, c->bb[9], 512, true));
   RC(conv1(c, B[B_C42], 0, B[B_C43], 0, c->bb[10], 256, true));
   RC(conv1(c, B[B_C43], 0, B[B_CAT], kCatFeat, c->bb[11], 128, true));
+  // Stages 2-6 run their 7x7 layers on chunk-planar tensors when conv_m16_bf16x3 takes every 7x7
+  // launch of this geometry and the fused heads write the stage maps (OP_STAGE_PLANAR=0: the
+  // [pixel][channels] buffers, A/B aid): Mconv1..Mconv5 outputs in PA / PB, and the Mconv1 input
+  // (the 185-channel concat) in CATP -- the feature slice copied over from CAT once per forward
+  // (stage 1's conv5_1 reads it from CAT), every stage's (paf, heat) written there by its head.
+  static const bool planar_env = !(getenv("OP_STAGE_PLANAR") && atoi(getenv("OP_STAGE_PLANAR")) == 0);
+  const int sh8 = B[B_BRA].h, sw8 = B[B_BRA].w;
+  const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && planar_env && head_fused_on() &&
+                      conv_m16_takes(c->gn, sh8, sw8, 1, 256) && conv_m16_takes(c->gn, sh8, sw8, 2, 128);
+  if (planar)
+    RC(launch_split_to_planar(B[B_CAT].p, B[B_CATP].p, c->gn, sh8, sw8, B[B_CAT].pad, B[B_CAT].cs, 128 / 16,
+                              c->stream));
+  const Act& catm = planar ? B[B_CATP] : B[B_CAT];  // stage maps + Mconv1 input
   // stage 1 (CocoPoseNet.py:153-165)
   const Act& cat = B[B_CAT];
   Act s1 = B[B_S1];
@@ -847,27 +862,21 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   {
     const Act* m32 = (c->split && stages) ? &B[B_MAP32] : nullptr;
     const PackedConv a[2] = {c->s1_g[0][2], c->s1_g[1][2]}, b[2] = {c->s1_last[0], c->s1_last[1]};
-    const int h = head2(c, B[B_BRA], 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
+    const int h = head2(c, B[B_BRA], 0, 128, catm, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
     if (h > 0) return h;
     if (h < 0) {
       RC(conv2(c, B[B_BRA], 0, 128, s1, 0, 512, c->s1_g[0][2], c->s1_g[1][2], 512, 512, true));
-      RC(conv2(c, s1, 0, 512, cat, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false, m32, 0, 40));
+      RC(conv2(c, s1, 0, 512, catm, kCatPaf, kCatHeat, c->s1_last[0], c->s1_last[1], 40, 20, false, m32, 0, 40));
     }
     RC(dump_stage(0));
   }
-  // stages 2-6 (CocoPoseNet.py:167-260).  Mconv1..Mconv5 outputs go to the chunk-planar stage
-  // buffers when conv_m16_bf16x3 takes every 7x7 launch of this geometry and the fused head reads
-  // Mconv5's output (OP_STAGE_PLANAR=0: the [pixel][channels] buffers, A/B aid)
+  // stages 2-6 (CocoPoseNet.py:167-260), on the chunk-planar buffers when `planar` (above)
   Act s6 = B[B_S1];
   s6.cs = 256;  // Mconv6 output reuses the stage-1 1x1 buffer (no halo) with a 256-channel stride
-  static const bool planar_env = !(getenv("OP_STAGE_PLANAR") && atoi(getenv("OP_STAGE_PLANAR")) == 0);
-  const int sh8 = B[B_BRA].h, sw8 = B[B_BRA].w;
-  const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && planar_env && head_fused_on() &&
-                      conv_m16_takes(c->gn, sh8, sw8, 1, 256) && conv_m16_takes(c->gn, sh8, sw8, 2, 128);
   const Act& SA = planar ? B[B_PA] : B[B_BRA];
   const Act& SB = planar ? B[B_PB] : B[B_BRB];
   for (int st = 0; st < 5; ++st) {
-    RC(conv1(c, cat, 0, SA, 0, c->st_first[st], 256, true));
+    RC(conv1(c, catm, 0, SA, 0, c->st_first[st], 256, true));
     const Act* src = &SA;
     const Act* dst = &SB;
     c->prof_join = true;  // Mconv2..Mconv5 follow Mconv1 back to back on the stream
@@ -883,11 +892,11 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
     // the last stage also leaves a dense f32 copy (paf at 0, heat at 40) for the post-process
     const Act* m32 = (c->split && (st == 4 || stages)) ? &B[B_MAP32] : nullptr;
     const PackedConv a[2] = {c->st_g[st][0][4], c->st_g[st][1][4]}, b[2] = {c->st_last[st][0], c->st_last[st][1]};
-    const int h = head2(c, *src, 0, 128, cat, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
+    const int h = head2(c, *src, 0, 128, catm, kCatPaf, kCatHeat, a, b, 40, 20, m32, 0, 40);
     if (h > 0) return h;
     if (h < 0) {
       RC(conv2(c, *src, 0, 128, s6, 0, 128, c->st_g[st][0][4], c->st_g[st][1][4], 128, 128, true));
-      RC(conv2(c, s6, 0, 128, cat, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false, m32, 0,
+      RC(conv2(c, s6, 0, 128, catm, kCatPaf, kCatHeat, c->st_last[st][0], c->st_last[st][1], 40, 20, false, m32, 0,
                40));
     }
     RC(dump_stage(st + 1));

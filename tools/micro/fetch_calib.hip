@@ -34,6 +34,18 @@ __global__ __launch_bounds__(CHUNK / 16 * 64) void fetch_case(const char* src, l
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+// chunk-planar halo (round 3, conv_m16_bf16x3's stage buffers): wave w reads 64 consecutive 16-B
+// pieces of plane w, the 4 planes `plane` bytes apart (a 1-KiB run per wave instruction)
+__global__ __launch_bounds__(256) void fetch_planar(const char* src, long plane, long groups) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (long g = blockIdx.x; g < groups; g += gridDim.x) {
+    const char* p = src + wave * plane + (g * 64 + lane) * 16L;
+    __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + wave * 1024), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 // streams a separate 1 GiB buffer between cases (evicts the Infinity Cache)
 __global__ __launch_bounds__(256) void flush(const float4* p, long n, float* sink) {
   float4 a = {0, 0, 0, 0};
@@ -75,6 +87,16 @@ int main() {
   run<512, 64>(buf, known);    // 7x7 halo: 64-B chunk of a 512-B (128-channel) pixel
   run<256, 64>(buf, known / 2);  // 64-B chunk of a 256-B (64-channel) pixel
   run<512, 128>(buf, known / 2);  // 3x3 halo: 128-B chunk pair of a 512-B pixel
+  {
+    const long nflush = (1L << 30) / 16;
+    hipLaunchKernelGGL(flush, dim3(4096), dim3(256), 0, 0, (const float4*)g_flush, nflush, g_sink);
+    CK(hipDeviceSynchronize());
+    const long plane = (long)(known / 4), groups = plane / 1024;
+    hipLaunchKernelGGL(fetch_planar, dim3(2048), dim3(256), 4096, 0, buf, plane, groups);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    printf("fetch_planar: 4 planes x %ld B, known bytes %zu (%.1f MB)\n", plane, known, known / 1e6);
+  }
   CK(hipFree(buf));
   CK(hipFree(g_flush));
   return 0;

@@ -1,12 +1,14 @@
 """Summarise a tools/profile.sh run into profiles/<tag>.md + profiles/<tag>_traffic.json.
 
-HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from
-separate --pmc passes (KiB units).  On gfx950 FETCH_SIZE reads half the bytes of a wide coalesced
-16-B/lane stream (the guide's calibration, doubled here by default); the conv kernels' halo loads
-are not streams, so their factor comes from our own calibration on a known byte count
-(tools/micro/fetch_calib.hip, profiles/fetch_calib_r01.md): a 64-B channel chunk of each pixel
-record (conv_m16_bf16x3's 7x7 halo) is counted at x0.98 of its bytes, a 128-B chunk pair
-(conv_m16k_bf16x3's 3x3 halo) at x1.12.
+HBM (fabric) traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes (KiB units), and FETCH_SIZE is doubled.  Round 3 measured why, per
+kernel (tools/gpu_tcc_bytes.sh, profiles/r03/tcc_r03g_request_sizes.txt): every read request our
+kernels and the calibration micro-benchmark send to the fabric is a 128-B request
+(TCC_EA0_RDREQ_128B == TCC_EA0_RDREQ), and FETCH_SIZE's formula counts 128-B requests through
+TCC_BUBBLE, which stays 0, i.e. at 64 B each.  Rounds 1-2 applied x0.98 / x1.12 to the conv halo
+patterns from tools/micro/fetch_calib.hip, which compared FETCH_SIZE with the bytes the kernel USED;
+a 64-B chunk of a 128-B line still moves the whole line, so those factors under-reported the conv
+kernels' traffic by about 2x (profiles/fetch_calib_r03.md).
 usage: python tools/summarize_profile.py gpurun_out/prof_<tag> <tag>
 """
 import csv
@@ -31,17 +33,8 @@ def pmc(d, sub, counter):
     return acc
 
 
-# FETCH_SIZE -> bytes, by kernel (dominant read pattern); default: the guide's 16-B/lane stream
-# (round 3: conv_m16s loads its halo in the 7x7 pattern, conv_m16r in the 3x3 chunk-pair pattern;
-# their register weight fragments are L2 hits after the first workgroup and barely reach FETCH_SIZE)
-FETCH_FACTOR = (("conv_m16_bf16x3", 536870912 / 545724096), ("conv_m16s_bf16x3", 536870912 / 545724096),
-                ("conv_m16k_bf16x3", 268435456 / 240281984), ("conv_m16r_bf16x3", 268435456 / 240281984))
-
-
+# FETCH_SIZE -> bytes: every read request is 128 B, tallied at 64 B (see the docstring)
 def fetch_factor(name):
-    for prefix, f in FETCH_FACTOR:
-        if short(name).replace("op::", "").startswith(prefix):
-            return f
     return 2.0
 
 
@@ -66,7 +59,7 @@ def main():
              "Bench line of the stats pass: value %.1f frames/s, ms/step %.2f, dtype %s, batch %s." % (
                  bench.get("value", 0), bench.get("ms_per_step", 0), bench.get("dtype"),
                  bench.get("config", {}).get("frames_per_step_per_gpu")), "",
-             "| kernel | calls | avg us | total % | HBM read MB/launch (FETCH x calibrated factor) | HBM write MB/launch |",
+             "| kernel | calls | avg us | total % | HBM read MB/launch (FETCH_SIZE x 2: 128-B requests) | HBM write MB/launch |",
              "|---|---|---|---|---|---|"]
     traffic = {}
     for r in stats:
