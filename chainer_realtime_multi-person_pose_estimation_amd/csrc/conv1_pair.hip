@@ -60,6 +60,9 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const halo = lds;                           // 8 planes x 340 slots x 16 B
   float* const inw = (float*)(lds + 8 * kP1Plane);  // [3][12][36] f32, planar: lanes read consecutive words
+  // cv2 LINEAR taps of the window's 36 columns and 12 rows, computed once per workgroup (f64 scale
+  // arithmetic) instead of once per staged pixel
+  LinTap* const taps = (LinTap*)(lds + 8 * kP1Plane + kP1IR * kP1IC * 12);  // [36 x][12 y]
   const int n = blockIdx.z;
   const int y0 = blockIdx.y * kP1R, x0 = blockIdx.x * kP1C;
   const int tid = threadIdx.x;
@@ -68,6 +71,11 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
   const int l16 = lane & 15, kg = lane >> 4;
   const int csel = kg >> 1, khalf = kg & 1;
 
+  if constexpr (FROM_FRAMES) {
+    if (tid < kP1IC) taps[tid] = cv_linear_tap(x0 - 2 + tid, w, sw, true);
+    else if (tid < kP1IC + kP1IR) taps[tid] = cv_linear_tap(y0 - 2 + tid - kP1IC, h, sh, false);
+    __syncthreads();
+  }
   // ---- network-input window (zero outside the image: conv1_1's padding) ----
   for (int i = tid; i < kP1IR * kP1IC; i += 256) {
     const int iy = i / kP1IC, ix = i - (i / kP1IC) * kP1IC;
@@ -76,8 +84,8 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
     if (gy >= 0 && gy < h && gx >= 0 && gx < w) {
       if constexpr (FROM_FRAMES) {
         const uint8_t* src = frames + (int64_t)n * frame_bytes;
-        const LinTap tx = cv_linear_tap(gx, w, sw, true);
-        const LinTap ty = cv_linear_tap(gy, h, sh, false);
+        const LinTap tx = taps[ix];
+        const LinTap ty = taps[kP1IC + iy];
 #pragma unroll
         for (int c = 0; c < 3; ++c) v[c] = p1_recon(cv_linear_px(src, row_stride, sh, sw, tx, ty, c));
       } else {  // padded split16 input (h+2, w+2, 16): channels 0..7 hi at +0, lo at +16
@@ -125,9 +133,11 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
     __syncthreads();  // input window staged / the previous half's MFMAs are done with the halo
 #if C1P_MFMA11
     // ---- conv1_1 for channels 32*half .. +31 on the 10 x 34 window -> split LDS planes, on MFMA:
-    // K = the 27 (tap, input channel) products + 5 zeros, im2col fragments built in registers from
-    // the staged window, three bf16 products per MAC like every other layer (round 3: the f32 VALU
-    // form below took ~75 % of the workgroup's MFMA time in issue slots) ----
+    // K = the 27 (tap, input channel) products, then the bias (B = 1.0, A = b11: the bias rides in
+    // the accumulation instead of a per-block load + add) and 4 zeros; im2col fragments built in
+    // registers from the staged window with unconditional reads (a slot past the window reads its
+    // last slot and is not stored); three bf16 products per MAC like every other layer (round 3:
+    // the f32 VALU form below took ~75 % of the workgroup's MFMA time in issue slots) ----
     {
       bf16x8p a11h[2], a11l[2];
 #pragma unroll
@@ -136,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 8 * kg + j;
-          const float v = k < 27 ? wt11[k * 64 + co] : 0.0f;
+          const float v = k < 27 ? wt11[k * 64 + co] : (k == 27 ? b11[co] : 0.0f);
           const __bf16 h = (__bf16)v;
           a11h[cb][j] = h;
           a11l[cb][j] = (__bf16)(v - (float)h);
@@ -144,22 +154,23 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
       }
       for (int blk = wave; blk < (kP1Slots + 15) / 16; blk += 4) {
         const int sl = blk * 16 + l16;  // window slot = halo slot (row-major, pitch kP1HC)
-        const int ry = sl / kP1HC, rx = sl - (sl / kP1HC) * kP1HC;
+        const int slc = min(sl, kP1Slots - 1);
+        const int ry = slc / kP1HC, rx = slc - (slc / kP1HC) * kP1HC;
+        const float* const px = inw + ry * kP1IC + rx;
         bf16x8p bh, bl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 8 * kg + j;
-          float v = 0.0f;
-          if (k < 27 && sl < kP1Slots) {
-            const int t = k / 3, ci = k - (k / 3) * 3;
-            v = inw[ci * kP1IR * kP1IC + (ry + t / 3) * kP1IC + rx + t % 3];
-          }
+          const int kk = k < 27 ? k : 0;
+          const int t = kk / 3, ci = kk - (kk / 3) * 3;
+          float v = px[ci * kP1IR * kP1IC + (t / 3) * kP1IC + t % 3];
+          v = k < 27 ? v : (k == 27 ? 1.0f : 0.0f);
           const __bf16 h = (__bf16)v;
           bh[j] = h;
           bl[j] = (__bf16)(v - (float)h);
         }
         const int gy = y0 - 1 + ry, gx = x0 - 1 + rx;
-        const bool inside = sl < kP1Slots && gy >= 0 && gy < h && gx >= 0 && gx < w;
+        const bool inside = gy >= 0 && gy < h && gx >= 0 && gx < w;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           floatx4 d = {0.f, 0.f, 0.f, 0.f};
@@ -171,8 +182,7 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
           u16x4p hv, lv;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float f = __fadd_rn(d[e], b11[32 * half + 16 * cb + 4 * kg + e]);
-            f = f > 0.0f && inside ? f : 0.0f;
+            const float f = d[e] > 0.0f && inside ? d[e] : 0.0f;
             const __bf16 hh = (__bf16)f;
             hv[e] = __builtin_bit_cast(unsigned short, hh);
             lv[e] = __builtin_bit_cast(unsigned short, (__bf16)(f - (float)hh));
@@ -322,7 +332,7 @@ int launch_conv1_pair(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
     set_error("conv1_pair: odd map size");
     return OP_ERR_INVALID;
   }
-  const int lds = 8 * kP1Plane + kP1IR * kP1IC * 12;
+  const int lds = 8 * kP1Plane + kP1IR * kP1IC * 12 + (kP1IC + kP1IR) * (int)sizeof(LinTap);
   static bool attr = false;
   if (!attr) {
     OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv1_pair_bf16x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
