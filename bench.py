@@ -112,7 +112,8 @@ MFMA_7X7 = {4: "v_mfma_f32_16x16x32_bf16", 5: "v_mfma_f32_16x16x32_bf16", 6: "v_
 
 def committed_traffic(kernel, batch, precision, halo_mode):
     """HBM bytes per launch (read + write) of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/**/*_traffic.json, FETCH_SIZE x calibrated pattern factor + WRITE_SIZE,
+    summary (profiles/**/*_traffic.json: FETCH_SIZE x 2 -- every fabric read request is 128 B and
+    FETCH_SIZE tallies it at 64 B, profiles/fetch_calib_r03.md -- + WRITE_SIZE,
     tools/summarize_profile.py) taken on this exact workload; (None, None) when none matches."""
     import glob
     best = None
