@@ -28,7 +28,7 @@ EXPORTED = (
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_upload_wait", "op_conv_census", "op_host_alloc", "op_host_free",
     "op_pack_results", "op_comm_unique_id", "op_comm_create", "op_comm_destroy", "op_comm_gather_results",
     "op_comm_wait", "op_comm_overflow", "op_comm_overflow_result", "op_detect_precise", "op_resize_cubic",
-    "op_set_conv_algo", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
+    "op_set_conv_algo", "op_set_stage_layout", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
@@ -87,6 +87,7 @@ def lib():
         "op_detect": ([P, P, I32, I32, I64, P, P, I32, P], ctypes.c_int),
         "op_detect_precise": ([P, P, I32, I32, I64, P, P, I32, P, P, P], ctypes.c_int),
         "op_set_conv_algo": ([P, I32], ctypes.c_int),
+        "op_set_stage_layout": ([P, I32], ctypes.c_int),
         "op_set_batch_invariant": ([P, I32], ctypes.c_int),
         "op_profile_classes": ([P, I32], ctypes.c_int),
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
@@ -218,7 +219,8 @@ def layer_table():
 
 
 CENSUS = {"7x7_splitk": 11, "7x7_other": 12, "3x3_w48": 13, "3x3_w32": 14, "3x3_pool": 15, "3x3_splitk": 16,
-          "3x3_big": 17, "conv1_pair": 18, "3x3_r256": 19, "3x3_r128": 20, "3x3_r_pool": 21}
+          "3x3_big": 17, "conv1_pair": 18, "3x3_r256": 19, "3x3_r128": 20, "3x3_r_pool": 21,
+          "7x7_planar": 22}
 CENSUS_SLOTS = 24
 
 
@@ -306,6 +308,11 @@ class Context(object):
     def set_conv_algo(self, algo):
         """Kernel family of the bf16x3 convolutions (include/openpose_hip.h: op_set_conv_algo)."""
         check(lib().op_set_conv_algo(self.h, int(algo)), "op_set_conv_algo")
+
+    def set_stage_layout(self, planar):
+        """Chunk-planar (1, default) or [row][col][channels] (0) 7x7 stage tensors
+        (include/openpose_hip.h: op_set_stage_layout); the maps are bit-identical either way."""
+        check(lib().op_set_stage_layout(self.h, 1 if planar else 0), "op_set_stage_layout")
 
     def set_batch_invariant(self, enable=True):
         """One accumulation order for every batch size (include/openpose_hip.h: op_set_batch_invariant);

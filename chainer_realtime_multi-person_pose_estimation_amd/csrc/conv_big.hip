@@ -892,6 +892,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
       census_add(npx);
       if (tl.ksplit > 1) census_add(OP_CENSUS_7X7_SPLITK);
+      if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
       const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
       if (rc != OP_OK) return rc;
       if (tl.ksplit > 1) {

@@ -286,6 +286,7 @@ struct op_ctx {
   bool split = true;           // 3xBF16 split convs (default) or exact f32 MFMA convs
   bool gsplit = true;          // format the arena is currently carved for
   int conv_algo = 4;           // split-path conv kernel family (op_set_conv_algo)
+  int stage_planar = 1;        // chunk-planar 7x7 stage tensors where conv_m16 takes them (op_set_stage_layout)
   Act buf[B_COUNT];
   // post-process
   PostBuffers pb{};
@@ -841,13 +842,12 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   RC(conv1(c, B[B_C42], 0, B[B_C43], 0, c->bb[10], 256, true));
   RC(conv1(c, B[B_C43], 0, B[B_CAT], kCatFeat, c->bb[11], 128, true));
   // Stages 2-6 run their 7x7 layers on chunk-planar tensors when conv_m16_bf16x3 takes every 7x7
-  // launch of this geometry and the fused heads write the stage maps (OP_STAGE_PLANAR=0: the
-  // [pixel][channels] buffers, A/B aid): Mconv1..Mconv5 outputs in PA / PB, and the Mconv1 input
+  // launch of this geometry and the fused heads write the stage maps (op_set_stage_layout(ctx, 0)
+  // or OP_STAGE_PLANAR=0: the [pixel][channels] buffers): Mconv1..Mconv5 outputs in PA / PB, and the Mconv1 input
   // (the 185-channel concat) in CATP -- the feature slice copied over from CAT once per forward
   // (stage 1's conv5_1 reads it from CAT), every stage's (paf, heat) written there by its head.
-  static const bool planar_env = !(getenv("OP_STAGE_PLANAR") && atoi(getenv("OP_STAGE_PLANAR")) == 0);
   const int sh8 = B[B_BRA].h, sw8 = B[B_BRA].w;
-  const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && planar_env && head_fused_on() &&
+  const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && c->stage_planar && head_fused_on() &&
                       conv_m16_takes(c->gn, sh8, sw8, 1, 256) && conv_m16_takes(c->gn, sh8, sw8, 2, 128);
   if (planar)
     RC(launch_split_to_planar(B[B_CAT].p, B[B_CATP].p, c->gn, sh8, sw8, B[B_CAT].pad, B[B_CAT].cs, 128 / 16,
@@ -1273,6 +1273,7 @@ int op_create(const op_params* params, const op_limits* limits, int device, op_c
     if (m == 0 || m == 3 || m == 4 || m == 5) op::g_halo_mode = m;
   }
   c->conv_algo = op::g_halo_mode;
+  c->stage_planar = !(getenv("OP_STAGE_PLANAR") && atoi(getenv("OP_STAGE_PLANAR")) == 0);
   if (const char* e = getenv("OP_DEBUG_SYNC")) op::g_debug_sync = e[0] == '1';
   if (const char* e = getenv("OP_GUARD")) op::g_guard = ((size_t)atol(e) + 255) / 256 * 256;
   // scipy _gaussian_kernel1d(sigma, 0, int(4*sigma + 0.5)) taps (restated; pinned by the tests)
@@ -2753,6 +2754,18 @@ int op_set_batch_invariant(op_ctx* c, int32_t enable) {
     c->gexec = nullptr;
   }
   c->splitk = sk;
+  return OP_OK;
+}
+
+int op_set_stage_layout(op_ctx* c, int32_t planar) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  c->stage_planar = planar ? 1 : 0;
+  if (c->gexec) {  // captured launches bake in the buffers
+    OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
   return OP_OK;
 }
 

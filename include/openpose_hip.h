@@ -108,6 +108,13 @@ int op_get_precision(op_ctx* ctx, int32_t* mode);
  * halos, rectangular 7x7 tap pairs, register weights -- live in git history: tools/build_rev.sh
  * builds that revision as an A/B variant.) */
 int op_set_conv_algo(op_ctx* ctx, int32_t algo);
+/* Layout of the 7x7 stage tensors of stages 2-6 (default 1; env OP_STAGE_PLANAR=0 sets new
+ * contexts to 0).  1: chunk-planar ([16-channel chunk][hi/lo plane][row][col] per frame) wherever
+ * the 7x7 kernel conv_m16 takes every 7x7 launch of the geometry -- its halo loads are then
+ * contiguous runs (about half the HBM reads); 0: [row][col][channels].  Same kernels, same
+ * arithmetic and order: the maps are bit-identical either way.  No reference counterpart (the
+ * reference's tensors live in Chainer/cuDNN). */
+int op_set_stage_layout(op_ctx* ctx, int32_t planar);
 /* Batch invariance (default off).  A launch that fills few CUs (one frame, one crop) splits the
  * 7x7 convolutions' input channels over several workgroups and sums their f32 partials, so a
  * frame's maps then differ from the same frame inside a larger batch by f32 re-association (~1e-5;
@@ -280,6 +287,7 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_3X3_R256 19    /* conv_m16r_bf16x3<8, ...> (register weights, 256 channels per workgroup) */
 #define OP_CENSUS_3X3_R128 20    /* conv_m16r_bf16x3<4, ...> (128 channels per workgroup) */
 #define OP_CENSUS_3X3_R_POOL 21  /* conv_m16r_bf16x3<., ., ., true> (fused 2x2 max-pool) */
+#define OP_CENSUS_7X7_PLANAR 22  /* 7x7 launches on chunk-planar tensors (op_set_stage_layout) */
 #define OP_CENSUS_SLOTS 24
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

@@ -196,3 +196,23 @@ def test_precise_staged_batch_of_16_equals_single_frames(lib):
                 assert np.array_equal(got[i][0], single[0]) and np.array_equal(got[i][1], single[1]), i
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n", [1, 38])
+def test_planar_stage_layout_is_bit_identical(lib, bctx, n):
+    """op_set_stage_layout: the 7x7 stage tensors of stages 2-6 in the chunk-planar layout (the
+    default; conv_m16 halo loads as contiguous runs) or [row][col][channels] -- the same kernels
+    and accumulation order, so the maps agree bit for bit; the census shows which layout ran."""
+    rng = np.random.default_rng(500 + n)
+    x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
+    out = {}
+    for planar in (1, 0):
+        bctx.set_stage_layout(planar)
+        try:
+            _census_npx(lib)
+            out[planar] = bctx.forward(x)
+            cen = _census_npx(lib)
+        finally:
+            bctx.set_stage_layout(1)
+        assert cen["7x7_planar"] == (25 if planar else 0), (planar, cen)
+    assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
