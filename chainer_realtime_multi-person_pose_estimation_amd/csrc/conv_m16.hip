@@ -48,19 +48,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int co0 = (unit - grp * tl.co_tiles) * CW;
   const SplitConvGroup g = grp == 0 ? g0 : g1;
   if (co0 >= g.cop) return;
-  int P0, P1;
-  if (tl.fa_tiles) {  // frame-aligned raster tiles (wide maps): one frame per tile, last one partial
-    const int f = widx / tl.fa_tiles;
-    P0 = f * tl.hw + (widx - f * tl.fa_tiles) * CAP;
-    P1 = min(P0 + CAP, (f + 1) * tl.hw) - 1;
-  } else {
-    P0 = widx * CAP;
-    P1 = min(P0 + CAP, tl.total) - 1;
-  }
-  const int frame = P0 / tl.hw;
-  const int y0 = (P0 - frame * tl.hw) / s.w;
-  const int fb = P1 / tl.hw;
-  const int rowsA = fb != frame ? s.h - y0 + 2 * R : (1 << 30);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -72,8 +59,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int wp_in = s.w + 2 * s.pin;
   const int hp_in = s.h + 2 * s.pin;
   const int64_t pix_bytes = (int64_t)s.cs_in * 4;
-  const char* const fbase = (const char*)g.in + (int64_t)frame * hp_in * wp_in * pix_bytes;
-  const char* const fbase_b = (const char*)g.in + (int64_t)fb * hp_in * wp_in * pix_bytes;
   // a chunk's 4 halo planes: 16-B pieces of each pixel record, or (chunk-planar input) 4 planes of
   // contiguous rows, so each wave's 64 x 16 B read is one 1-KiB run
   const int64_t in_pc = split_piece_stride(s.in_planar, hp_in, wp_in);
@@ -101,138 +86,173 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
   };
 
-  // this lane's pixel of each block -> byte offset of its halo slot in its hi plane (2 khalf), so
-  // a B fragment address is qb[pb] + the tap's offset: one VALU add per block
-  int qb[NPX];
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    int q = 0;
-    if (P <= P1) {
-      const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
-      const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
-      q = (f == frame ? y - y0 : rowsA + y) * tl.pitch + x;
+  // the tile's geometry: pixels [P0, P1] of the batch, frame / first row, the second frame's rows
+  struct Tile {
+    int P0, P1, frame, y0, fb, rowsA;
+  };
+  auto tile_of = [&](int widx) {
+    Tile T;
+    if (tl.fa_tiles) {  // frame-aligned raster tiles (wide maps): one frame per tile, last one partial
+      const int f = widx / tl.fa_tiles;
+      T.P0 = f * tl.hw + (widx - f * tl.fa_tiles) * CAP;
+      T.P1 = min(T.P0 + CAP, (f + 1) * tl.hw) - 1;
+    } else {
+      T.P0 = widx * CAP;
+      T.P1 = min(T.P0 + CAP, tl.total) - 1;
     }
-    qb[pb] = (2 * khalf) * HPLANE + q * 16;
-  }
-
-  floatx4 acc[4][NPX];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
-  const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
+    T.frame = T.P0 / tl.hw;
+    T.y0 = (T.P0 - T.frame * tl.hw) / s.w;
+    T.fb = T.P1 / tl.hw;
+    T.rowsA = T.fb != T.frame ? s.h - T.y0 + 2 * R : (1 << 30);
+    // wave-uniform: keep them in SGPRs (the compiler divides on the VALU)
+    T.P0 = __builtin_amdgcn_readfirstlane(T.P0);
+    T.P1 = __builtin_amdgcn_readfirstlane(T.P1);
+    T.frame = __builtin_amdgcn_readfirstlane(T.frame);
+    T.y0 = __builtin_amdgcn_readfirstlane(T.y0);
+    T.fb = __builtin_amdgcn_readfirstlane(T.fb);
+    T.rowsA = __builtin_amdgcn_readfirstlane(T.rowsA);
+    return T;
+  };
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
-  int it = cb0 * KSQP;
-  for (int c = cb0; c < cb1; ++c) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    {
-      const char* src0 = fbase + (int64_t)(c * 4 + h_plane) * in_pc;
-      const char* src0_b = fbase_b + (int64_t)(c * 4 + h_plane) * in_pc;
-      int hr = h_r0, hc = h_c0;
-      char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
-      for (int i = h_i0; i < tl.nh; i += 2) {
-        const bool in_a = hr < rowsA;
-        const int yy = min((in_a ? y0 - R + hr : hr - rowsA - R) + s.pin, hp_in - 1);
-        const int xx = min(hc - R + s.pin, wp_in - 1);
-        glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * in_px), dst);
-        dst += 2 * 1024;
-        hc += 2 * 64;
-        while (hc >= tl.pitch) {
-          hc -= tl.pitch;
-          ++hr;
+  // this wave's pieces of chunk c's halo (LDS-DMA)
+  auto issue_halo = [&](int c, const Tile& T) {
+    const char* const fbase = (const char*)g.in + (int64_t)T.frame * hp_in * wp_in * pix_bytes;
+    const char* const fbase_b = (const char*)g.in + (int64_t)T.fb * hp_in * wp_in * pix_bytes;
+    const char* src0 = fbase + (int64_t)(c * 4 + h_plane) * in_pc;
+    const char* src0_b = fbase_b + (int64_t)(c * 4 + h_plane) * in_pc;
+    int hr = h_r0, hc = h_c0;
+    char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
+    for (int i = h_i0; i < tl.nh; i += 2) {
+      const bool in_a = hr < T.rowsA;
+      const int yy = min((in_a ? T.y0 - R + hr : hr - T.rowsA - R) + s.pin, hp_in - 1);
+      const int xx = min(hc - R + s.pin, wp_in - 1);
+      glds16((const void*)((in_a ? src0 : src0_b) + (int64_t)(yy * wp_in + xx) * in_px), dst);
+      dst += 2 * 1024;
+      hc += 2 * 64;
+      while (hc >= tl.pitch) {
+        hc -= tl.pitch;
+        ++hr;
+      }
+    }
+  };
+  const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
+
+  const Tile T = tile_of(widx);
+#pragma unroll
+  for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
+  {
+    // this lane's pixel of each block -> byte offset of its halo slot in its hi plane (2 khalf), so
+    // a B fragment address is qb[pb] + the tap's offset: one VALU add per block
+    int qb[NPX];
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      const int P = T.P0 + (pg * NPX + pb) * 16 + l16;
+      int q = 0;
+      if (P <= T.P1) {
+        const int f = P / tl.hw, pp = P - (P / tl.hw) * tl.hw;
+        const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
+        q = (f == T.frame ? y - T.y0 : T.rowsA + y) * tl.pitch + x;
+      }
+      qb[pb] = (2 * khalf) * HPLANE + q * 16;
+    }
+
+    floatx4 acc[4][NPX];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    int it = cb0 * KSQP;
+    for (int c = cb0; c < cb1; ++c) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_halo(c, T);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      bf16x8g ah[4], al[4];
+#pragma unroll 1
+      for (int t = 0; t < KSQP; t += 2, it += 2) {
+        wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
+        __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
+        asm volatile("" ::: "memory");
+        stage_w(it + 2 * AHEAD);
+        stage_w(it + 2 * AHEAD + 1);
+        // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
+        // tap (zero weights) reads tap t's pixels: finite values, times zero
+        const int t1 = t + 1 < KSQ ? t + 1 : t;
+        const int toff0 = ((t / KS) * tl.pitch + (t - (t / KS) * KS)) * 16;
+        const int toff1 = ((t1 / KS) * tl.pitch + (t1 - (t1 / KS) * KS)) * 16;
+        const int toff = tsel ? toff1 : toff0;
+        const char* wsl = ring + ((unsigned)it % RING + tsel) * SLOT_W + wlane;  // it even: no wrap
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
+          al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
+        }
+        bf16x8g bh[2], bl[2];
+        bh[0] = *(const bf16x8g*)(halo + qb[0] + toff);
+        bl[0] = *(const bf16x8g*)(halo + qb[0] + toff + HPLANE);
+#pragma unroll
+        for (int pb = 0; pb < NPX; ++pb) {
+          const int cur = pb & 1;
+          if (pb + 1 < NPX) {
+            const char* bp = halo + qb[pb + 1] + toff;
+            bh[cur ^ 1] = *(const bf16x8g*)bp;
+            bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
+            acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          }
         }
       }
     }
     wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    bf16x8g ah[4], al[4];
-#pragma unroll 1
-    for (int t = 0; t < KSQP; t += 2, it += 2) {
-      wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
-      __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
-      asm volatile("" ::: "memory");
-      stage_w(it + 2 * AHEAD);
-      stage_w(it + 2 * AHEAD + 1);
-      // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
-      // tap (zero weights) reads tap t's pixels: finite values, times zero
-      const int t1 = t + 1 < KSQ ? t + 1 : t;
-      const int toff0 = ((t / KS) * tl.pitch + (t - (t / KS) * KS)) * 16;
-      const int toff1 = ((t1 / KS) * tl.pitch + (t1 - (t1 / KS) * KS)) * 16;
-      const int toff = tsel ? toff1 : toff0;
-      const char* wsl = ring + ((unsigned)it % RING + tsel) * SLOT_W + wlane;  // it even: no wrap
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        ah[cb] = *(const bf16x8g*)(wsl + cb * 256);
-        al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
-      }
-      bf16x8g bh[2], bl[2];
-      bh[0] = *(const bf16x8g*)(halo + qb[0] + toff);
-      bl[0] = *(const bf16x8g*)(halo + qb[0] + toff + HPLANE);
+
+    if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
+      const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
+      float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
-        const int cur = pb & 1;
-        if (pb + 1 < NPX) {
-          const char* bp = halo + qb[pb + 1] + toff;
-          bh[cur ^ 1] = *(const bf16x8g*)bp;
-          bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        const int P = T.P0 + (pg * NPX + pb) * 16 + l16;
+        if (P > T.P1) continue;
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+          if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
         }
       }
-    }
-  }
-  wait_vmcnt<0>();
-
-  if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
-    const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
-    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
+    } else {
+      const int wp_out = s.w + 2 * s.pout;
+      const int hp_out = s.h + 2 * s.pout;
+      const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
+      const int64_t out_px = split_pixel_stride(s.out_planar, s.cs_out);
 #pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) {
-      const int P = P0 + (pg * NPX + pb) * 16 + l16;
-      if (P > P1) continue;
+      for (int pb = 0; pb < NPX; ++pb) {
+        const int P = T.P0 + (pg * NPX + pb) * 16 + l16;
+        const int f = P / tl.hw, pp = P - f * tl.hw;
+        const int y = pp / s.w, x = pp - y * s.w;
+        char* optr = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
+                     ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * out_px;
+        float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-        if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
+        for (int cb = 0; cb < 4; ++cb) {
+          const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+          floatx4 v;
+          uint32_t own[4], w[4];
+          split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f},
+                          s.relu, v, own, w);
+          if (P > T.P1 || co >= g.cout_store) continue;
+          store_split_group(optr, co, kg, g.cout_store, own, w, out_pc);
+          if (o32) *(floatx4*)(o32 + co) = v;
+        }
       }
-    }
-    return;
-  }
-  const int wp_out = s.w + 2 * s.pout;
-  const int hp_out = s.h + 2 * s.pout;
-  const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
-  const int64_t out_px = split_pixel_stride(s.out_planar, s.cs_out);
-#pragma unroll
-  for (int pb = 0; pb < NPX; ++pb) {
-    const int P = P0 + (pg * NPX + pb) * 16 + l16;
-    const int f = P / tl.hw, pp = P - f * tl.hw;
-    const int y = pp / s.w, x = pp - y * s.w;
-    char* optr = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
-                 ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * out_px;
-    float* o32 = g.out32 ? g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off : nullptr;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-      floatx4 v;
-      uint32_t own[4], w[4];
-      split_pair_swap(acc[cb][pb], co < g.cop ? *(const floatx4*)(g.bias + co) : floatx4{0.f, 0.f, 0.f, 0.f}, s.relu,
-                      v, own, w);
-      if (P > P1 || co >= g.cout_store) continue;
-      store_split_group(optr, co, kg, g.cout_store, own, w, out_pc);
-      if (o32) *(floatx4*)(o32 + co) = v;
     }
   }
 }
