@@ -428,8 +428,9 @@ def main():
             "frames_over_caps_rerun": (gather.g.overflow_caps - ovc0) if gather.device else None,
             "overflow_ms_per_step": round(ovs / (vsteps + 1) * 1e3, 3),
             "note": "post-process on the random network's own last-stage maps (noise peaks); frames whose record "
-                    "cannot carry the whole result travel as overflow: past 64 persons their kept rows are "
-                    "copied, over the batched caps they are re-run alone uncapped, on the host's collect path "
+                    "cannot carry the whole result travel as overflow: past 64 persons their rows are written "
+                    "by the device into page-locked host memory when the records are packed, over the batched "
+                    "caps they are re-run alone uncapped, on the host's collect path "
                     "(counted over the warm-up and timed steps)"}
         if args.maps == "synthetic":
             ctx.use_staged_maps(True)

@@ -238,12 +238,23 @@ struct KeepSlot {
   int maxs = 0;
   int32_t* cnt = nullptr;
   size_t cnt_cap = 0;
-  int32_t* d_hdr = nullptr;  // n x {status, n_peaks, n_persons, why: 0 whole record, 1 over the caps, 2 > max_persons}
+  // n x kKeepHdr {status, n_peaks, n_persons, why: 0 whole record, 1 over the caps, 2 > max_persons,
+  // offset of the frame's rows in h_rows (doubles; -1: not there, read them from res)}
+  int32_t* d_hdr = nullptr;
   int32_t* h_hdr = nullptr;  // pinned copy, complete when the slot's gather is
   size_t hdr_cap = 0;
+  // rows of the frames past max_persons written by keep_overflow straight into page-locked host
+  // memory (poses then scores per frame, packed by a device counter), so collecting them needs no
+  // GPU copy: a copy on any stream would share a hardware queue with the next steps' compute
+  // and wait for them (round 3: 65 ms per 114-frame step on the network-maps line)
+  double* h_rows = nullptr;
+  double* d_rows_view = nullptr;  // the device's address of h_rows (hipHostGetDevicePointer)
+  int64_t h_rows_cap = 0;  // doubles
+  int32_t* d_rows_cnt = nullptr;
   PostRecord rec{};
   int n = 0;
 };
+constexpr int kKeepHdr = 5;  // int32 per frame in KeepSlot::d_hdr / h_hdr
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
@@ -1338,6 +1349,8 @@ int op_destroy(op_ctx* c) {
   if (c->host_stage) hipHostFree(c->host_stage);
   if (c->up_pinned) hipHostFree(c->up_pinned);
   for (auto& k : c->keep) {
+    if (k.h_rows) hipHostFree(k.h_rows);
+    if (k.d_rows_cnt) hipFree(k.d_rows_cnt);
     if (k.maps) hipFree(k.maps);
     if (k.res) hipFree(k.res);
     if (k.cnt) hipFree(k.cnt);
@@ -2253,9 +2266,11 @@ int op_fetch_maps(op_ctx* c, int32_t first, int32_t n, float* pafs, float* heatm
 // Record of frame i: int32 {status, n_peaks, n_persons, 0}, int64 global frame id, 8 pad bytes,
 // then max_persons x 54 f64 poses and max_persons f64 scores (rows past n_persons zero).
 __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, int max_persons, int64_t frame_base,
-                                                    int frame_stride, char* __restrict__ out, int64_t rec_bytes) {
+                                                    int frame_stride, char* __restrict__ out, int64_t rec_bytes,
+                                                    int32_t* __restrict__ rows_cnt) {
   const int i = blockIdx.x;
   const int f = first + i;
+  if (rows_cnt && i == 0 && threadIdx.x == 0) *rows_cnt = 0;  // keep_overflow's row allocator
   char* r = out + (int64_t)i * rec_bytes;
   const int status = b.res_hdr[4 * f];
   const int persons = status == OP_OK ? b.res_hdr[4 * f + 2] : 0;
@@ -2284,23 +2299,37 @@ int64_t record_bytes(int max_persons) { return 32 + (int64_t)max_persons * 55 * 
 // result rows (they are complete: copied out as they are).
 __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, int max_persons, const float* __restrict__ src,
                                                      int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
-                                                     double* __restrict__ res, int32_t* __restrict__ hdr) {
+                                                     double* __restrict__ res, int32_t* __restrict__ hdr,
+                                                     double* __restrict__ h_rows, int64_t h_rows_cap,
+                                                     int32_t* __restrict__ rows_cnt) {
   const int i = blockIdx.x;
   const int f = first + i;
   const int status = b.res_hdr[4 * f];
   const int persons = b.res_hdr[4 * f + 2];
   const int why = status == OP_ERR_CAPACITY ? 1 : (status == OP_OK && persons > max_persons) ? 2 : 0;
+  __shared__ int off_s;
   if (threadIdx.x == 0) {
-    hdr[4 * i] = status;
-    hdr[4 * i + 1] = b.res_hdr[4 * f + 1];
-    hdr[4 * i + 2] = status == OP_OK ? persons : 0;
-    hdr[4 * i + 3] = why;
+    int off = -1;
+    if (why == 2) {  // rows -> page-locked host memory, if the slot's capacity holds them
+      const int o = atomicAdd(rows_cnt, persons * 55);
+      if ((int64_t)o + persons * 55 <= h_rows_cap) off = o;
+    }
+    off_s = off;
+    hdr[kKeepHdr * i] = status;
+    hdr[kKeepHdr * i + 1] = b.res_hdr[4 * f + 1];
+    hdr[kKeepHdr * i + 2] = status == OP_OK ? persons : 0;
+    hdr[kKeepHdr * i + 3] = why;
+    hdr[kKeepHdr * i + 4] = off;
   }
+  __syncthreads();
   if (why == 2) {
     const double* ps = b.res_poses + (int64_t)f * b.maxs * 54;
-    double* d = res + (int64_t)i * b.maxs * 55;
+    const double* ss = b.res_scores + (int64_t)f * b.maxs;
+    const int off = off_s;
+    double* d = off >= 0 ? h_rows + off : res + (int64_t)i * b.maxs * 55;
+    const int64_t sc = off >= 0 ? (int64_t)persons * 54 : (int64_t)b.maxs * 54;
     for (int e = threadIdx.x; e < persons * 54; e += 256) d[e] = ps[e];
-    for (int e = threadIdx.x; e < persons; e += 256) d[(int64_t)b.maxs * 54 + e] = b.res_scores[(int64_t)f * b.maxs + e];
+    for (int e = threadIdx.x; e < persons; e += 256) d[sc + e] = ss[e];
     return;
   }
   if (why != 1 || !src) return;
@@ -2319,8 +2348,27 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     set_error("pack records: bad frame range");
     return OP_ERR_INVALID;
   }
+  int32_t* rows_cnt = nullptr;
+  if (keep_slot >= 0) {
+    KeepSlot& k = c->keep[keep_slot];
+    if (!k.d_rows_cnt) OP_HIP_CHECK(hipMalloc((void**)&k.d_rows_cnt, sizeof(int32_t)));
+    // page-locked rows for frames past max_persons: 256 persons per frame on average (the rest,
+    // if ever, are read from the device copy in res)
+    const int64_t want = (int64_t)n * 256 * 55;
+    if (want > k.h_rows_cap) {
+      OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      if (k.h_rows) OP_HIP_CHECK(hipHostFree(k.h_rows));
+      k.h_rows = nullptr;
+      k.h_rows_cap = 0;
+      // coherent (fine-grained): the kernel's stores go straight to host memory
+      OP_HIP_CHECK(hipHostMalloc((void**)&k.h_rows, (size_t)want * 8, hipHostMallocMapped | hipHostMallocCoherent));
+      OP_HIP_CHECK(hipHostGetDevicePointer((void**)&k.d_rows_view, k.h_rows, 0));
+      k.h_rows_cap = want;
+    }
+    rows_cnt = k.d_rows_cnt;
+  }
   hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
-                     frame_stride, (char*)dst, record_bytes(max_persons));
+                     frame_stride, (char*)dst, record_bytes(max_persons), rows_cnt);
   OP_AFTER_LAUNCH("pack_records", c->stream);
   if (keep_slot >= 0) {
     KeepSlot& k = c->keep[keep_slot];
@@ -2333,7 +2381,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     }
     RC(grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)n * c->pb.maxs * 55 * 8, "keep_res"));
     k.maxs = c->pb.maxs;
-    const size_t hb = (size_t)n * 16;
+    const size_t hb = (size_t)n * kKeepHdr * 4;
     if (hb > k.hdr_cap) {
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
       if (k.d_hdr) OP_HIP_CHECK(hipFree(k.d_hdr));
@@ -2346,7 +2394,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.hdr_cap = hb;
     }
     hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                       k.maps, k.cnt, k.res, k.d_hdr);
+                       k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.h_rows_cap, k.d_rows_cnt);
     OP_AFTER_LAUNCH("keep_overflow", c->stream);
     OP_HIP_CHECK(hipMemcpyAsync(k.h_hdr, k.d_hdr, hb, hipMemcpyDeviceToHost, c->stream));
     k.rec = r;
@@ -2371,10 +2419,10 @@ int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t* reasons, in
   const KeepSlot& k = c->keep[slot];
   int m = 0;
   for (int i = 0; i < k.n; ++i)
-    if (k.h_hdr[4 * i + 3]) {
+    if (k.h_hdr[kKeepHdr * i + 3]) {
       if (m < cap) {
         frames[m] = i;
-        if (reasons) reasons[m] = k.h_hdr[4 * i + 3];
+        if (reasons) reasons[m] = k.h_hdr[kKeepHdr * i + 3];
       }
       ++m;
     }
@@ -2390,18 +2438,25 @@ int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* score
   }
   KeepSlot& k = c->keep[slot];
   memset(res, 0, sizeof(*res));
-  if (!k.h_hdr[4 * frame + 3]) {
+  const int32_t* hd = k.h_hdr + kKeepHdr * frame;
+  if (!hd[3]) {
     set_error("kept result: the frame's record carries its whole result");
     return OP_ERR_STATE;
   }
-  if (k.h_hdr[4 * frame + 3] == 2) {  // complete batched rows, kept as they were
-    const int p = k.h_hdr[4 * frame + 2];
+  if (hd[3] == 2) {  // complete batched rows, kept as they were
+    const int p = hd[2];
     res->status = OP_OK;
-    res->n_peaks = k.h_hdr[4 * frame + 1];
+    res->n_peaks = hd[1];
     res->n_persons = p;
     if (p > cap) {
       set_error("result capacity too small");
       return OP_ERR_CAPACITY;
+    }
+    if (hd[4] >= 0) {  // written to page-locked memory by keep_overflow (complete: the gather waited)
+      const double* h = k.h_rows + hd[4];
+      memcpy(poses, h, (size_t)p * 54 * 8);
+      memcpy(scores, h + (size_t)p * 54, (size_t)p * 8);
+      return OP_OK;
     }
     const double* d = k.res + (size_t)frame * k.maxs * 55;
     OP_HIP_CHECK(hipMemcpy(poses, d, (size_t)p * 54 * 8, hipMemcpyDeviceToHost));
