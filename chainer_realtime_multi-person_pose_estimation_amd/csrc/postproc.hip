@@ -116,14 +116,26 @@ __global__ __launch_bounds__(256) void resize_planar(const float* __restrict__ x
 struct PafLow {
   LowMap m;
   int lh, lw, mh, mw, off;
+  const AxisTap* ty = nullptr;  // per-block LDS tables of axis_tap over the map rows / columns
+  const AxisTap* tx = nullptr;  // (round 3: the f64 linspace divisions once per block, not per sample)
   __device__ __forceinline__ float at(int c, int y, int x) const {
     return up_sample(m, off + c, up_tap(y, x, lh, lw, mh, mw));
+  }
+  // both channels of limb l at one map pixel: one tap for the pair
+  __device__ __forceinline__ void at2(int c, int y, int x, float& v0, float& v1) const {
+    const UpTap t = ty ? up_tap2(ty[y], tx[x]) : up_tap(y, x, lh, lw, mh, mw);
+    v0 = up_sample(m, off + c, t);
+    v1 = up_sample(m, off + c + 1, t);
   }
 };
 struct PafFull {  // planar (38, mh, mw) of one frame (limb_pairs_full offsets p per frame)
   const float* p;
   int mh, mw;
   __device__ __forceinline__ float at(int c, int y, int x) const { return p[((int64_t)c * mh + y) * mw + x]; }
+  __device__ __forceinline__ void at2(int c, int y, int x, float& v0, float& v1) const {
+    v0 = at(c, y, x);
+    v1 = at(c + 1, y, x);
+  }
 };
 
 __device__ __forceinline__ int peak_count(const int32_t* cnt, int maxp) {
@@ -154,8 +166,9 @@ __device__ __forceinline__ void limb_pairs_body(const Paf& paf, const PostShape&
     for (int i = 0; i < np_; ++i) {
       const int yi = (int)rint(linspace_at(ay, by, np_, i));
       const int xi = (int)rint(linspace_at(ax, bx, np_, i));
-      const double px = (double)paf.at(2 * l, yi, xi);
-      const double py = (double)paf.at(2 * l + 1, yi, xi);
+      float fx, fy;
+      paf.at2(2 * l, yi, xi, fx, fy);
+      const double px = (double)fx, py = (double)fy;
       const double ip = __fma_rn(px, ux, __dmul_rn(py, uy));
       inner[i] = ip;
       nvalid += ip > s.inner_thresh ? 1 : 0;
@@ -189,9 +202,17 @@ __device__ __forceinline__ void limb_pairs_body(const Paf& paf, const PostShape&
   }
 }
 
-__global__ __launch_bounds__(256) void limb_pairs_low(MapSource src, PostShape s, PostBuffers b) {
+__global__ __launch_bounds__(256) void limb_pairs_low(MapSource src, PostShape s, PostBuffers b, int tables) {
   const int f = blockIdx.x, l = blockIdx.y;
+  extern __shared__ AxisTap tab[];  // tables: [mh] rows then [mw] columns
   PafLow paf;
+  if (tables) {
+    for (int i = threadIdx.x; i < s.mh + s.mw; i += 256)
+      tab[i] = i < s.mh ? axis_tap(i, s.lh, s.mh) : axis_tap(i - s.mh, s.lw, s.mw);
+    __syncthreads();
+    paf.ty = tab;
+    paf.tx = tab + s.mh;
+  }
   paf.m = low_map(src, s.lw, f);
   paf.lh = s.lh;
   paf.lw = s.lw;
@@ -216,11 +237,26 @@ __global__ __launch_bounds__(256) void limb_pairs_full(const float* __restrict__
 // the stably sorted list: every skipped candidate keeps a used endpoint forever.
 // kBig: the used-peak bitsets live in HBM (b.used, [frame][limb][2][words]) for any peak count;
 // otherwise in LDS (maxp <= 2048).
+// block-wide int sum over 256 threads (4 waves); red: 4 ints of LDS
+__device__ __forceinline__ int block_sum_i(int v, int* red, int tid) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+constexpr int kGreedySort = 4096;  // candidates per (frame, limb) sorted in LDS (48 KiB); more: argmax scans
+
 template <bool kBig>
 __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
   __shared__ unsigned used_lds[kBig ? 1 : 128];
   __shared__ double red_s[4];
   __shared__ int red_i[4];
+  __shared__ unsigned long long skey[kGreedySort];  // sorted batches: score bits
+  __shared__ int32_t sq[kGreedySort];               // and candidate (pair) indices
+  __shared__ unsigned long long samp[256];          // sorted sample of the keys (K > kGreedySort)
+  __shared__ int fill_n, got_s;
   const int f = blockIdx.x, l = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ja = s.limbs[l][0], jb = s.limbs[l][1];
@@ -249,6 +285,150 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
   const double* cs = b.cand_score + fl * b.maxc;
   const int32_t* ci = b.cand_idx + fl * b.maxc;
   int got = 0;
+  if (K > 0) {
+    // round 3: first-fit over the candidates in (score desc, index asc) order (positive doubles
+    // order like their bit patterns), taken in batches of keys [T, hi) that fit kGreedySort LDS
+    // slots: a batch is collected by one scan, bitonic-sorted in LDS, and walked by one wave 64
+    // candidates at a time -- each accepted candidate kills the later lanes that share one of its
+    // peaks (a ballot per acceptance).  Thresholds T come from a sorted sample of 256 keys; a batch
+    // that would still overflow (ties) hands the rest to the argmax scans below, which continue
+    // correctly: every candidate of a finished batch is accepted or has a used endpoint.
+    unsigned long long hi = ~0ull;  // exclusive upper key bound of the next batch
+    int r = 0;                      // sample rank of the last threshold
+    if (K > kGreedySort) {
+      samp[tid] = (unsigned long long)__double_as_longlong(cs[(int)(((int64_t)tid * K) / 256)]);
+      __syncthreads();
+      for (int k = 2; k <= 256; k <<= 1)  // descending
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const int p = tid ^ j;
+          const unsigned long long a = samp[tid], c = samp[p];
+          __syncthreads();
+          if (p > tid ? (((tid & k) == 0) ? a < c : a > c) : (((p & k) == 0) ? c < a : c > a)) samp[tid] = c;
+          __syncthreads();
+        }
+    }
+    bool done = false;
+    while (!done) {
+      // this batch's threshold: all the rest if it fits, else the sample rank whose count fits
+      unsigned long long T = 0;
+      int cnt = 0;
+      if (K > kGreedySort) {
+        int step = (int)((int64_t)kGreedySort * 256 * 3 / 4 / K);
+        step = step < 1 ? 1 : step;
+        for (;;) {
+          int j = r + step;
+          if (j >= 256) {
+            T = 0;
+          } else {
+            while (j < 256 && samp[j] >= hi) ++j;  // ties with the previous threshold
+            T = j < 256 ? samp[j] : 0ull;
+          }
+          int c = 0;
+          for (int i = tid; i < K; i += 256) {
+            const unsigned long long key = (unsigned long long)__double_as_longlong(cs[i]);
+            c += (key >= T && key < hi) ? 1 : 0;
+          }
+          c = block_sum_i(c, red_i, tid);
+          if (c <= kGreedySort) {
+            cnt = c;
+            r = j < 256 ? j : 256;
+            break;
+          }
+          if (step == 1) {
+            cnt = -1;  // a tie run longer than a batch: the argmax scans take over
+            break;
+          }
+          step >>= 1;
+        }
+        if (cnt < 0) break;
+      } else {
+        cnt = K;
+      }
+      // collect the batch (any order; sorted next)
+      if (tid == 0) fill_n = 0;
+      __syncthreads();
+      if (K <= kGreedySort) {
+        for (int i = tid; i < K; i += 256) {
+          skey[i] = (unsigned long long)__double_as_longlong(cs[i]);
+          sq[i] = ci[i];
+        }
+      } else {
+        for (int i = tid; i < K; i += 256) {
+          const unsigned long long key = (unsigned long long)__double_as_longlong(cs[i]);
+          if (key >= T && key < hi) {
+            const int slot = atomicAdd(&fill_n, 1);
+            skey[slot] = key;
+            sq[slot] = ci[i];
+          }
+        }
+      }
+      int n2 = 1;
+      while (n2 < cnt) n2 <<= 1;
+      for (int i = cnt + tid; i < n2; i += 256) {
+        skey[i] = 0ull;  // padding sorts last
+        sq[i] = 0x7fffffff;
+      }
+      __syncthreads();
+      for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < n2; i += 256) {
+            const int p = i ^ j;
+            if (p > i) {
+              const unsigned long long ki = skey[i], kp = skey[p];
+              const int qi = sq[i], qp = sq[p];
+              const bool i_first = ki > kp || (ki == kp && qi < qp);
+              if (((i & k) == 0) != i_first) {
+                skey[i] = kp;
+                skey[p] = ki;
+                sq[i] = qp;
+                sq[p] = qi;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      if (wave == 0) {
+        for (int c0 = 0; c0 < cnt && got < lim; c0 += 64) {
+          const int i = c0 + lane;
+          int ia = -1, ib = -1;
+          bool alive = false;
+          if (i < cnt) {
+            const int q = sq[i];
+            ia = q / nb;
+            ib = q - ia * nb;
+            alive = !((used_a[ia >> 5] >> (ia & 31)) & 1u) && !((used_b[ib >> 5] >> (ib & 31)) & 1u);
+          }
+          unsigned long long m = __ballot(alive);
+          while (m && got < lim) {
+            const int jl = __ffsll((long long)m) - 1;
+            const int ja_ = __shfl(ia, jl), jb_ = __shfl(ib, jl);
+            if (lane == jl || ia == ja_ || ib == jb_) alive = false;
+            if (lane == 0) {
+              used_a[ja_ >> 5] |= 1u << (ja_ & 31);
+              used_b[jb_ >> 5] |= 1u << (jb_ & 31);
+              const int64_t o = fl * b.maxp + got;
+              b.conn_ab[2 * o] = base_a + ja_;
+              b.conn_ab[2 * o + 1] = base_b + jb_;
+              b.conn_score[o] = __longlong_as_double((long long)skey[c0 + jl]);
+            }
+            if constexpr (kBig) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // HBM bitsets: the
+            ++got;                                                                     // next chunk reads them
+            m = __ballot(alive);
+          }
+        }
+        if (lane == 0) got_s = got;
+      }
+      __syncthreads();
+      got = got_s;
+      done = T == 0 || got >= lim;
+      hi = T;
+      __syncthreads();  // skey / sq / fill_n are rewritten by the next batch
+    }
+    if (done) {
+      if (tid == 0) b.conn_cnt[fl] = got;
+      return;
+    }
+  }
   while (got < lim && K > 0) {
     double best = -1.0;  // every kept candidate has score > 0
     int bidx = 0x7fffffff;
@@ -836,7 +1016,11 @@ int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, h
   hs.mw = s.mw;
   if ((rc = run_heat_tiled(hs, s, b, st))) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
-  hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, pair_blocks(b)), dim3(256), 0, st, src, s, b);
+  // axis-tap tables in LDS when they fit 48 KiB (368 x 368 maps: 17 KiB; 1280 x 720: 47 KiB)
+  const size_t tab = (size_t)(s.mh + s.mw) * sizeof(AxisTap);
+  const int tables = tab <= 48 * 1024 ? 1 : 0;
+  hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, pair_blocks(b)), dim3(256), tables ? tab : 0, st, src, s, b,
+                     tables);
   OP_AFTER_LAUNCH("limb_pairs_low", st);
   if ((rc = launch_greedy(s, b, st))) return rc;
   if ((rc = launch_group(s, b, st))) return rc;
