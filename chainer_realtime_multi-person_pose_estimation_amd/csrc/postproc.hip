@@ -118,14 +118,22 @@ struct PafLow {
   int lh, lw, mh, mw, off;
   const AxisTap* ty = nullptr;  // per-block LDS tables of axis_tap over the map rows / columns
   const AxisTap* tx = nullptr;  // (round 3: the f64 linspace divisions once per block, not per sample)
+  const float* p0 = nullptr;    // the limb's two low-res PAF planes staged in LDS ([lh][lw] each)
+  const float* p1 = nullptr;
   __device__ __forceinline__ float at(int c, int y, int x) const {
     return up_sample(m, off + c, up_tap(y, x, lh, lw, mh, mw));
   }
   // both channels of limb l at one map pixel: one tap for the pair
   __device__ __forceinline__ void at2(int c, int y, int x, float& v0, float& v1) const {
     const UpTap t = ty ? up_tap2(ty[y], tx[x]) : up_tap(y, x, lh, lw, mh, mw);
-    v0 = up_sample(m, off + c, t);
-    v1 = up_sample(m, off + c + 1, t);
+    if (p0) {
+      const int i = t.v0 * lw + t.u0;
+      v0 = up_combine(t, p0[i], p0[i + 1], p0[i + lw], p0[i + lw + 1]);
+      v1 = up_combine(t, p1[i], p1[i + 1], p1[i + lw], p1[i + lw + 1]);
+    } else {
+      v0 = up_sample(m, off + c, t);
+      v1 = up_sample(m, off + c + 1, t);
+    }
   }
 };
 struct PafFull {  // planar (38, mh, mw) of one frame (limb_pairs_full offsets p per frame)
@@ -202,18 +210,38 @@ __device__ __forceinline__ void limb_pairs_body(const Paf& paf, const PostShape&
   }
 }
 
+constexpr int64_t kPairsStage = 2048;  // candidate pairs of a (frame, limb) from which limb_pairs_low stages
+
 __global__ __launch_bounds__(256) void limb_pairs_low(MapSource src, PostShape s, PostBuffers b, int tables) {
   const int f = blockIdx.x, l = blockIdx.y;
-  extern __shared__ AxisTap tab[];  // tables: [mh] rows then [mw] columns
+  extern __shared__ AxisTap tab[];  // tables: [mh] rows then [mw] columns; then (tables 2) the planes
+  // this block's share of the limb's candidate pairs; the LDS tables / planes only where the pairs
+  // repay their set-up (crowded frames), sparse frames sample the L2-resident map directly
+  const int na = peak_count(b.peak_cnt + (int64_t)f * OP_N_JOINTS + s.limbs[l][0], b.maxp);
+  const int nb = peak_count(b.peak_cnt + (int64_t)f * OP_N_JOINTS + s.limbs[l][1], b.maxp);
+  const int64_t npairs = (int64_t)na * nb;
+  if ((int64_t)blockIdx.z * blockDim.x >= npairs) return;
+  if (npairs < kPairsStage) tables = 0;
   PafLow paf;
   if (tables) {
     for (int i = threadIdx.x; i < s.mh + s.mw; i += 256)
       tab[i] = i < s.mh ? axis_tap(i, s.lh, s.mh) : axis_tap(i - s.mh, s.lw, s.mw);
-    __syncthreads();
     paf.ty = tab;
     paf.tx = tab + s.mh;
   }
   paf.m = low_map(src, s.lw, f);
+  if (tables == 2) {  // this limb's two PAF channels of the frame's low-res map -> LDS
+    float* pl = (float*)(tab + s.mh + s.mw);
+    const int area = s.lh * s.lw;
+    for (int i = threadIdx.x; i < area; i += 256) {
+      const int y = i / s.lw, x = i - (i / s.lw) * s.lw;
+      pl[i] = paf.m.at(src.paf_off + 2 * l, y, x);
+      pl[area + i] = paf.m.at(src.paf_off + 2 * l + 1, y, x);
+    }
+    paf.p0 = pl;
+    paf.p1 = pl + area;
+  }
+  if (tables) __syncthreads();
   paf.lh = s.lh;
   paf.lw = s.lw;
   paf.mh = s.mh;
@@ -1016,9 +1044,18 @@ int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, h
   hs.mw = s.mw;
   if ((rc = run_heat_tiled(hs, s, b, st))) return rc;
   OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
-  // axis-tap tables in LDS when they fit 48 KiB (368 x 368 maps: 17 KiB; 1280 x 720: 47 KiB)
-  const size_t tab = (size_t)(s.mh + s.mw) * sizeof(AxisTap);
-  const int tables = tab <= 48 * 1024 ? 1 : 0;
+  // axis-tap tables in LDS when they fit 48 KiB (368 x 368 maps: 17 KiB; 1280 x 720: 47 KiB), and
+  // the limb's two low-res PAF planes next to them when both fit 64 KiB (46 x 46: +17 KiB): the
+  // 80 map reads per candidate pair hit LDS instead of scattered L2 lines
+  size_t tab = (size_t)(s.mh + s.mw) * sizeof(AxisTap);
+  const size_t planes = (size_t)2 * s.lh * s.lw * sizeof(float);
+  const int tables = tab + planes <= 64 * 1024 ? 2 : tab <= 48 * 1024 ? 1 : 0;
+  if (tables == 2) tab += planes;
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)limb_pairs_low, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr = true;
+  }
   hipLaunchKernelGGL(limb_pairs_low, dim3(s.n, OP_N_LIMBS, pair_blocks(b)), dim3(256), tables ? tab : 0, st, src, s, b,
                      tables);
   OP_AFTER_LAUNCH("limb_pairs_low", st);
