@@ -265,15 +265,6 @@ __global__ __launch_bounds__(256) void limb_pairs_full(const float* __restrict__
 // the stably sorted list: every skipped candidate keeps a used endpoint forever.
 // kBig: the used-peak bitsets live in HBM (b.used, [frame][limb][2][words]) for any peak count;
 // otherwise in LDS (maxp <= 2048).
-// block-wide int sum over 256 threads (4 waves); red: 4 ints of LDS
-__device__ __forceinline__ int block_sum_i(int v, int* red, int tid) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  __syncthreads();
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
-}
-
 constexpr int kGreedySort = 4096;  // candidates per (frame, limb) sorted in LDS (48 KiB); more: argmax scans
 
 template <bool kBig>
@@ -351,12 +342,33 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
             while (j < 256 && samp[j] >= hi) ++j;  // ties with the previous threshold
             T = j < 256 ? samp[j] : 0ull;
           }
-          int c = 0;
-          for (int i = tid; i < K; i += 256) {
-            const unsigned long long key = (unsigned long long)__double_as_longlong(cs[i]);
-            c += (key >= T && key < hi) ? 1 : 0;
+          // count and collect in one scan (a wave reserves its lanes' slots with one LDS atomic);
+          // a batch past the cap is dropped and the step halves
+          if (tid == 0) fill_n = 0;
+          __syncthreads();
+          for (int i0 = 0; i0 < K; i0 += 256) {
+            const int i = i0 + tid;
+            unsigned long long key = 0;
+            bool in = false;
+            if (i < K) {
+              key = (unsigned long long)__double_as_longlong(cs[i]);
+              in = key >= T && key < hi;
+            }
+            const unsigned long long m = __ballot(in);
+            int base = 0;
+            if (m) {
+              if (lane == 0) base = atomicAdd(&fill_n, __popcll(m));
+              base = __shfl(base, 0);
+            }
+            const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (in && slot < kGreedySort) {
+              skey[slot] = key;
+              sq[slot] = ci[i];
+            }
           }
-          c = block_sum_i(c, red_i, tid);
+          __syncthreads();
+          const int c = fill_n;
+          __syncthreads();
           if (c <= kGreedySort) {
             cnt = c;
             r = j < 256 ? j : 256;
@@ -372,22 +384,11 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
       } else {
         cnt = K;
       }
-      // collect the batch (any order; sorted next)
-      if (tid == 0) fill_n = 0;
-      __syncthreads();
+      // the batch (any order; sorted next): collected by the counting scan, or all K at once
       if (K <= kGreedySort) {
         for (int i = tid; i < K; i += 256) {
           skey[i] = (unsigned long long)__double_as_longlong(cs[i]);
           sq[i] = ci[i];
-        }
-      } else {
-        for (int i = tid; i < K; i += 256) {
-          const unsigned long long key = (unsigned long long)__double_as_longlong(cs[i]);
-          if (key >= T && key < hi) {
-            const int slot = atomicAdd(&fill_n, 1);
-            skey[slot] = key;
-            sq[slot] = ci[i];
-          }
         }
       }
       int n2 = 1;
