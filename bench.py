@@ -222,18 +222,28 @@ class Gather(object):
 
 
 def make_gather(Fr, ctx, transport, world):
+    g, err = None, None
     try:
         g = Fr.RcclGather(ctx, transport, GATHER_PERSONS, timeout=300.0)
+    except Exception as e:  # labelled, never silent: the line says which transport ran
+        err = e
+    if world > 1:
+        # one transport for every rank: if the communicator came up on some ranks only, all of them
+        # take the TCP gather (a rank left on RCCL would wait for peers that never join)
+        failed = transport.all_reduce(0.0 if err is None else 1.0, "sum")
+        if failed > 0 and g is not None:
+            g.close()
+            g, err = None, "%d rank(s) could not create the RCCL communicator" % int(failed)
+    if g is not None:
         if world == 1:
             return Gather(g, True, "single GPU (results packed in HBM, copied to pinned memory on a side "
                                    "stream, collected one step behind)")
         return Gather(g, True, "frame-parallel x%d, RCCL ncclGather of per-frame result records from HBM to "
                                "rank 0" % world)
-    except Exception as e:  # labelled, never silent: the line says which transport ran
-        if world == 1:
-            return Gather(None, False, "single GPU (synchronous result fetch: RCCL unavailable: %s)" % e)
-        return Gather(Fr.HostGather(transport, GATHER_PERSONS), False,
-                      "frame-parallel x%d, TCP gather of result records (RCCL init failed: %s)" % (world, e))
+    if world == 1:
+        return Gather(None, False, "single GPU (synchronous result fetch: RCCL unavailable: %s)" % err)
+    return Gather(Fr.HostGather(transport, GATHER_PERSONS), False,
+                  "frame-parallel x%d, TCP gather of result records (RCCL init failed: %s)" % (world, err))
 
 
 def measure(run, ctx, transport, steps, warmup, prof_7x7):

@@ -156,3 +156,43 @@ def test_count_persons_and_merge_with_overflow():
     back = F.unpack_full(F.pack_full(res))
     for a, b in zip(back, res):
         assert a[:3] == b[:3] and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+
+
+def _make_gather_rank(rank, world, port, q):
+    """bench.make_gather with an RCCL communicator that comes up on rank 0 only (stand-in)."""
+    try:
+        sys.path.insert(0, REPO)
+        import bench
+        Fr = pkg_module("frames")
+        closed = []
+
+        class FakeRccl(object):
+            def __init__(self, ctx, transport, max_persons, timeout=0.0):
+                if transport.rank != 0:
+                    raise RuntimeError("ncclCommInitRankConfig failed (test stand-in)")
+
+            def close(self):
+                closed.append(True)
+
+        Fr.RcclGather = FakeRccl
+        t = Fr.SocketTransport(rank, world, port=port, timeout=30.0)
+        g = bench.make_gather(Fr, None, t, world)
+        q.put((rank, type(g.g).__name__, g.device, bool(closed), "TCP gather" in g.label))
+        t.close()
+    except Exception as e:  # reported to the parent
+        q.put((rank, "error", repr(e)))
+
+
+def test_bench_gather_transport_is_one_for_all_ranks():
+    """A communicator that comes up on some ranks only: every rank takes the labelled TCP gather and
+    the ranks that had RCCL close it (bench.make_gather), instead of a split transport that hangs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_make_gather_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert got == [(0, "HostGather", False, True, True), (1, "HostGather", False, False, True)], got
