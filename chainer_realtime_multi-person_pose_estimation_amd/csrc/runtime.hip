@@ -250,6 +250,7 @@ struct KeepSlot {
   double* h_rows = nullptr;
   double* d_rows_view = nullptr;  // the device's address of h_rows (hipHostGetDevicePointer)
   int64_t h_rows_cap = 0;  // doubles
+  int64_t rows_cap_now = 0;  // of them, usable by the current pack (OP_KEEP_ROWS_AVG)
   int32_t* d_rows_cnt = nullptr;
   PostRecord rec{};
   int n = 0;
@@ -2353,8 +2354,12 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     KeepSlot& k = c->keep[keep_slot];
     if (!k.d_rows_cnt) OP_HIP_CHECK(hipMalloc((void**)&k.d_rows_cnt, sizeof(int32_t)));
     // page-locked rows for frames past max_persons: 256 persons per frame on average (the rest,
-    // if ever, are read from the device copy in res)
-    const int64_t want = (int64_t)n * 256 * 55;
+    // if ever, are read from the device copy in res; OP_KEEP_ROWS_AVG overrides the 256, 0 sends
+    // every such frame through the device copy -- a test aid)
+    const char* avg_env = getenv("OP_KEEP_ROWS_AVG");
+    const int64_t avg = avg_env ? std::max(0, atoi(avg_env)) : 256;
+    const int64_t want = (int64_t)n * avg * 55;
+    k.rows_cap_now = std::min(want, k.h_rows_cap);
     if (want > k.h_rows_cap) {
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
       if (k.h_rows) OP_HIP_CHECK(hipHostFree(k.h_rows));
@@ -2364,6 +2369,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       OP_HIP_CHECK(hipHostMalloc((void**)&k.h_rows, (size_t)want * 8, hipHostMallocMapped | hipHostMallocCoherent));
       OP_HIP_CHECK(hipHostGetDevicePointer((void**)&k.d_rows_view, k.h_rows, 0));
       k.h_rows_cap = want;
+      k.rows_cap_now = want;
     }
     rows_cnt = k.d_rows_cnt;
   }
@@ -2394,7 +2400,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.hdr_cap = hb;
     }
     hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                       k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.h_rows_cap, k.d_rows_cnt);
+                       k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt);
     OP_AFTER_LAUNCH("keep_overflow", c->stream);
     OP_HIP_CHECK(hipMemcpyAsync(k.h_hdr, k.d_hdr, hb, hipMemcpyDeviceToHost, c->stream));
     k.rec = r;
