@@ -162,22 +162,64 @@ int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t ss
 // resize_cubic_f32_planar, without writing and re-reading the running sum once per scale.
 // Channels 0..npaf-1 are the PAF map (its own cv2.resize call: SIMD/tail split over npaf
 // interleaved channels), npaf.. the heatmap (nheat channels).
+// Round 3: a block covers 256 outputs of one row for kMeanG consecutive channels; each thread makes
+// a scale's taps once and applies them to its kMeanG channels (scales outer, channels inner, one
+// running sum per channel, so every output's f32 operations and their order are unchanged): the
+// per-(pixel, channel) f64 tap arithmetic and 64-bit tap addressing were most of the instructions.
+constexpr int kMeanG = 8;
 __global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean(CubicMeanArgs a, float* __restrict__ dst, int dh,
                                                                     int dw, int npaf, int nheat) {
   const int x = blockIdx.x * 256 + threadIdx.x;
-  const int y = blockIdx.y, c = blockIdx.z;
+  const int y = blockIdx.y, c0 = blockIdx.z * kMeanG;
   if (x >= dw) return;
-  const bool paf = c < npaf;
-  const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
-  float sum = 0.0f;
+  const int nch = npaf + nheat;
+  float sum[kMeanG];
   for (int k = 0; k < a.ns; ++k) {
     const CubicTap tx = cv_cubic_tap_s(x, a.scx[k]);
     const CubicTap ty = cv_cubic_tap_s(y, a.scy[k]);
-    const float v = cv_cubic_f32(a.src[k], a.sstride[k], 1, a.sh[k], a.sw[k], c, tx, ty, x * cn + ce,
-                                 dw * cn / 4 * 4, a.cstride[k]);
-    sum = k == 0 ? v : __fadd_rn(sum, v);
+    const int sh = a.sh[k], sw = a.sw[k];
+    int64_t roff[4];
+    int col[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      roff[r] = (int64_t)clampc(ty.s - 1 + r, 0, sh - 1) * a.sstride[k];
+      col[r] = clampc(tx.s - 1 + r, 0, sw - 1);
+    }
+#pragma unroll
+    for (int g = 0; g < kMeanG; ++g) {
+      const int c = c0 + g;
+      if (c >= nch) break;
+      const bool paf = c < npaf;
+      const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+      const float* p = a.src[k] + (int64_t)c * a.cstride[k];
+      float hs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // cv_cubic_f32 (pstride 1): left-to-right horizontal sums
+        const float* row = p + roff[r];
+        float h = __fmul_rn(row[col[0]], tx.c[0]);
+        h = __fadd_rn(h, __fmul_rn(row[col[1]], tx.c[1]));
+        h = __fadd_rn(h, __fmul_rn(row[col[2]], tx.c[2]));
+        h = __fadd_rn(h, __fmul_rn(row[col[3]], tx.c[3]));
+        hs[r] = h;
+      }
+      float v;
+      if (x * cn + ce < dw * cn / 4 * 4) {  // its vertical orders (SIMD body / scalar tail)
+        const float t3 = __fmul_rn(hs[3], ty.c[3]);
+        const float t2 = __fadd_rn(__fmul_rn(hs[2], ty.c[2]), t3);
+        const float t1 = __fadd_rn(__fmul_rn(hs[1], ty.c[1]), t2);
+        v = __fadd_rn(__fmul_rn(hs[0], ty.c[0]), t1);
+      } else {
+        v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(hs[0], ty.c[0]), __fmul_rn(hs[1], ty.c[1])), __fmul_rn(hs[2], ty.c[2])),
+                      __fmul_rn(hs[3], ty.c[3]));
+      }
+      sum[g] = k == 0 ? v : __fadd_rn(sum[g], v);
+    }
   }
-  dst[((int64_t)c * dh + y) * dw + x] = __fdiv_rn(sum, (float)a.ns);
+  const int64_t plane = (int64_t)dh * dw;
+  float* o = dst + (int64_t)y * dw + x;
+#pragma unroll
+  for (int g = 0; g < kMeanG; ++g)
+    if (c0 + g < nch) o[(c0 + g) * plane] = __fdiv_rn(sum[g], (float)a.ns);
 }
 
 int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int32_t dh, int32_t dw, int32_t npaf,
@@ -187,7 +229,7 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
     return OP_ERR_INVALID;
   }
   hipLaunchKernelGGL(resize_cubic_f32_planar_mean, dim3((unsigned)((dw + 255) / 256), (unsigned)dh,
-                                                        (unsigned)(npaf + nheat)),
+                                                        (unsigned)((npaf + nheat + kMeanG - 1) / kMeanG)),
                      dim3(256), 0, st, a, dst, dh, dw, npaf, nheat);
   OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean", st);
   OP_HIP_CHECK(hipGetLastError());
