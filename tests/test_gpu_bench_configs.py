@@ -1,8 +1,9 @@
 """Parity at the configurations the bench itself runs (VERDICT r02 "next" item 1).
 
 The 7x7 stage kernel picks its raster-tile size per launch shape (conv_big.hip cost model): one
-frame -> NPX 2, 16 frames -> 5, 38 and 114 frames -> NPX 10 (640-px tiles; 114 frames = three
-rounds per launch), 57 frames -> NPX 8.  The headline (bench.py, 114 frames of 368x368 per step) and
+frame -> NPX 2, 16 frames -> 5, 38, 114 and 232 frames -> NPX 10 (640-px tiles; 232 frames = six
+full rounds per launch), 57 frames -> NPX 8.  The headline (bench.py, 232 frames of 368x368 per step
+since round 3's last A/B; 114 before) and
 the C4 line (16 frames of 1280x720) therefore run instantiations that batch <= 16 tests never reach.
 Here, at those exact batches:
 
@@ -51,7 +52,7 @@ def _max_err(a, b):
     return float(np.abs(np.float64(a) - np.float64(b)).max())
 
 
-@pytest.mark.parametrize("n,npx", [(38, 10), (57, 8), (114, 10)])
+@pytest.mark.parametrize("n,npx", [(38, 10), (57, 8), (114, 10), (232, 10)])
 def test_forward_at_bench_batches_vs_fixture_and_single_frames(lib, bctx, n, npx):
     """Both kernel sets at the bench's batches: conv algo 5 (conv_m16 raster tap pairs with NPX-block
     tiles, conv_m16k) and the default 4 (large 3x3 launches on the register-weight kernel
@@ -107,11 +108,12 @@ def test_forward_at_bench_batches_vs_fixture_and_single_frames(lib, bctx, n, npx
     assert np.array_equal(paf_d, paf) and np.array_equal(heat_d, heat)
 
 
-def test_staged_u8_path_at_the_headline_batch(lib, bctx):
-    """bench.py's own path and batch: 114 u8 368x368 frames through upload -> run_staged (fused
-    cv2-LINEAR resize + preprocess inside the conv1 pair, 92 convs, post-process)."""
-    n = 114
-    rng = np.random.default_rng(114)
+@pytest.mark.parametrize("n", [114, 232])
+def test_staged_u8_path_at_the_headline_batch(lib, bctx, n):
+    """bench.py's own path and batch: n u8 368x368 frames (232: the headline's batch; 114: round 3's
+    earlier one) through upload -> run_staged (fused cv2-LINEAR resize + preprocess inside the conv1
+    pair, 92 convs, post-process)."""
+    rng = np.random.default_rng(n)
     frames = rng.integers(0, 256, (n, SIDE, SIDE, 3), dtype=np.uint8)
     bctx.set_batch_invariant(True)
     try:
@@ -134,11 +136,11 @@ def test_staged_u8_path_at_the_headline_batch(lib, bctx):
         assert paf.shape == (n, 38, 46, 46) and heat.shape == (n, 19, 46, 46)
         # a border-spanning frame in the middle, and the two ends, against the CPU oracle
         W = case_weights("posenet", 0)
-        for i in (0, 57, n - 1):
+        for i in (0, n // 2, n - 1):
             x = cvresize.preprocess(cvresize.resize_linear_u8(frames[i], SIDE, SIDE))
             opaf, oheat = F.cocoposenet_forward(W, x)
             e = max(_max_err(paf[i], opaf[0]), _max_err(heat[i], oheat[0]))
-            print("staged batch 114 frame %d vs oracle: %.3g" % (i, e))
+            print("staged batch %d frame %d vs oracle: %.3g" % (n, i, e))
             assert e <= TOL, (i, e)
         # each frame == that frame staged alone
         for i in range(n):
