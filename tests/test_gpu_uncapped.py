@@ -122,3 +122,41 @@ def test_grouping_over_lds_subsets_and_int16_ids(ctx):
     assert len(want) == K
     got = ctx.grouping(conns, peaks)
     assert got.shape == want.shape and np.array_equal(got, want)
+
+
+def _tie_maps(step):
+    """46x46 maps with a lattice of equal bumps (one every `step` low-res pixels per joint) and an
+    exactly constant PAF field: candidate scores depend only on the pair's displacement, so the
+    limbs have thousands of candidates (more than limb_greedy's 4096-slot sorted batch) with long
+    runs of equal scores, resolved by enumeration order (pose_detector.py:172, stable sort)."""
+    heat = np.zeros((19, 46, 46), np.float32)
+    for j in range(18):
+        oy, ox = j % step, (j // step) % step
+        heat[j, oy::step, ox::step] = 0.8
+    paf = np.full((38, 46, 46), 0.3, np.float32)
+    return paf, heat
+
+
+@pytest.mark.parametrize("step", [3, 4])
+def test_greedy_ties_and_batches_vs_oracle(ctx, step):
+    """Round 3's limb_greedy (threshold batches sorted in LDS, one wave walking them) on tie-heavy
+    candidate lists: bit-exact with the oracle, alone and as one frame of a staged batch."""
+    paf, heat = _tie_maps(step)
+    want = _oracle_post(paf, heat, 368, 368)
+    if want is IndexError:
+        with pytest.raises(IndexError):
+            ctx.postprocess(paf, heat, 368, 368)
+        return
+    p, s, r = ctx.postprocess(paf, heat, 368, 368)
+    assert np.array_equal(p.reshape(want[0].shape), want[0]) and np.array_equal(s, want[1])
+    ctx.stage_frames(np.zeros((2, 368, 368, 3), np.uint8))
+    ctx.stage_maps(np.stack([np.concatenate([paf, heat])] * 2))
+    ctx.use_staged_maps(True)
+    try:
+        ctx.run_staged()
+        ctx.synchronize()
+        for i in range(2):
+            p, s, r = ctx.fetch_result(i)
+            assert np.array_equal(p.reshape(want[0].shape), want[0]) and np.array_equal(s, want[1]), i
+    finally:
+        ctx.use_staged_maps(False)
