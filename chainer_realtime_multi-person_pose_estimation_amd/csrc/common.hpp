@@ -194,6 +194,12 @@ int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, 
                             int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);
 int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
                             float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st);
+// mode 1 (planar destination) for n frames at once (source / destination frame strides in floats):
+// upsampling resizes (dh >= sh, dw >= sw) share each source row's horizontal sums among the output
+// rows of an 8-row block (round 3), the rest run resize_cubic_f32 per frame
+int launch_resize_cubic_f32_frames(const float* src, int64_t sstride, int32_t pstride, int64_t src_fstride, int32_t sh,
+                                   int32_t sw, int32_t cn, float* dst, int64_t dst_fstride, int32_t dh, int32_t dw,
+                                   int32_t n, hipStream_t st);
 // planar source (c*cstride + y*sstride + x) -> planar destination, modes 1-3 (precise.hip)
 // Per scale k: the padded-size map of one frame (planar, cstride floats per channel, sstride per
 // row), cropped to sh x sw, and the host-computed cubic scales to the output size.

@@ -116,6 +116,80 @@ int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, 
   return OP_OK;
 }
 
+// Mode 1 for upsampling resizes, n frames per launch (round 3): a block is 256 output columns x
+// kUpRows output rows of one (frame, channel).  Each thread makes the horizontal sums of the few
+// source rows those output rows need -- once, instead of once per output row as resize_cubic_f32
+// does -- keeps them in its own LDS column, then makes every output row's vertical sum from them.
+// The f32 operations of each output element are resize_cubic_f32's (cv_cubic_f32), in its order.
+constexpr int kUpRows = 8, kUpSrc = 8;
+__global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restrict__ src, int64_t sstride, int pstride,
+                                                           int64_t src_fstride, int sh, int sw, int cn,
+                                                           float* __restrict__ dst, int64_t dst_fstride, int dh, int dw,
+                                                           double scx, double scy) {
+  __shared__ float hsum[kUpSrc][256];
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y0 = blockIdx.y * kUpRows;
+  const int f = blockIdx.z / cn, c = blockIdx.z - (blockIdx.z / cn) * cn;
+  if (x >= dw) return;  // no barrier below: a thread reads only its own LDS column
+  const int ylast = min(y0 + kUpRows - 1, dh - 1);
+  const int r0 = cv_cubic_tap_s(y0, scy).s - 1;
+  const int nr = cv_cubic_tap_s(ylast, scy).s + 2 - r0 + 1;  // <= kUpSrc (the launcher checks)
+  const CubicTap tx = cv_cubic_tap_s(x, scx);
+  int64_t col[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) col[j] = (int64_t)clampc(tx.s - 1 + j, 0, sw - 1) * pstride;
+  const float* fs = src + (int64_t)f * src_fstride + c;
+  for (int r = 0; r < nr; ++r) {
+    const float* row = fs + (int64_t)clampc(r0 + r, 0, sh - 1) * sstride;
+    float h = __fmul_rn(row[col[0]], tx.c[0]);
+    h = __fadd_rn(h, __fmul_rn(row[col[1]], tx.c[1]));
+    h = __fadd_rn(h, __fmul_rn(row[col[2]], tx.c[2]));
+    h = __fadd_rn(h, __fmul_rn(row[col[3]], tx.c[3]));
+    hsum[r][threadIdx.x] = h;
+  }
+  const bool simd = x * cn + c < dw * cn / 4 * 4;
+  float* o = dst + (int64_t)f * dst_fstride + ((int64_t)c * dh + y0) * dw + x;
+  for (int y = y0; y <= ylast; ++y, o += dw) {
+    const CubicTap ty = cv_cubic_tap_s(y, scy);
+    const int b = ty.s - 1 - r0;
+    const float h0 = hsum[b][threadIdx.x], h1 = hsum[b + 1][threadIdx.x];
+    const float h2 = hsum[b + 2][threadIdx.x], h3 = hsum[b + 3][threadIdx.x];
+    float v;
+    if (simd) {
+      const float t3 = __fmul_rn(h3, ty.c[3]);
+      const float t2 = __fadd_rn(__fmul_rn(h2, ty.c[2]), t3);
+      const float t1 = __fadd_rn(__fmul_rn(h1, ty.c[1]), t2);
+      v = __fadd_rn(__fmul_rn(h0, ty.c[0]), t1);
+    } else {
+      v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty.c[0]), __fmul_rn(h1, ty.c[1])), __fmul_rn(h2, ty.c[2])),
+                    __fmul_rn(h3, ty.c[3]));
+    }
+    *o = v;
+  }
+}
+
+int launch_resize_cubic_f32_frames(const float* src, int64_t sstride, int32_t pstride, int64_t src_fstride, int32_t sh,
+                                   int32_t sw, int32_t cn, float* dst, int64_t dst_fstride, int32_t dh, int32_t dw,
+                                   int32_t n, hipStream_t st) {
+  const double scx = cv_cubic_scale(dw, sw), scy = cv_cubic_scale(dh, sh);
+  // source rows one block of kUpRows output rows needs: at most ceil((kUpRows - 1) * scy) + 1 + 3
+  const bool up = dh >= sh && dw >= sw && (int)((kUpRows - 1) * scy) + 5 <= kUpSrc;
+  if (!up) {
+    for (int f = 0; f < n; ++f) {
+      const int rc = launch_resize_cubic_f32(src + (int64_t)f * src_fstride, sstride, pstride, sh, sw, cn,
+                                             dst + (int64_t)f * dst_fstride, dh, dw, 1, 1.0f, st);
+      if (rc) return rc;
+    }
+    return OP_OK;
+  }
+  hipLaunchKernelGGL(resize_cubic_f32_up, dim3((unsigned)((dw + 255) / 256), (unsigned)((dh + kUpRows - 1) / kUpRows),
+                                               (unsigned)(cn * n)),
+                     dim3(256), 0, st, src, sstride, pstride, src_fstride, sh, sw, cn, dst, dst_fstride, dh, dw, scx, scy);
+  OP_AFTER_LAUNCH("resize_cubic_f32_up", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 // The same resize from a PLANAR source (element (y, x, c) at src[c*cstride + y*sstride + x]) into a
 // planar destination (modes 1-3 as above); block = 256 consecutive x of one (row, channel), so the
 // row's taps are block-uniform and the source rows are read coalesced.  Values identical to

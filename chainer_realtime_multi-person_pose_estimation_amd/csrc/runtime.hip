@@ -2665,16 +2665,18 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       paf_off = kCatPaf;
       heat_off = kCatHeat;
     }
-    for (int f = 0; f < n; ++f) {
-      const float* mf = mbase + f * mframe;
+    {
       // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping),
       // stored planar (cn, ph, pw) so the second resize reads coalesced rows; kept for every scale
-      // and frame until the fused second pass below
+      // and frame until the fused second pass below; every frame of the scale in one launch per map
       const int64_t pp = (int64_t)ph * pw;
-      float* mid_paf = c->d_pmid + mid_off[k] + (size_t)f * pp * (OP_N_PAF + OP_N_HEAT);
+      const int64_t mid_f = pp * (OP_N_PAF + OP_N_HEAT);
+      float* mid_paf = c->d_pmid + mid_off[k];
       float* mid_heat = mid_paf + (size_t)pp * OP_N_PAF;
-      RC(launch_resize_cubic_f32(mf + paf_off, mrow, mpx, lh, lw, OP_N_PAF, mid_paf, ph, pw, 1, 1.0f, c->stream));
-      RC(launch_resize_cubic_f32(mf + heat_off, mrow, mpx, lh, lw, OP_N_HEAT, mid_heat, ph, pw, 1, 1.0f, c->stream));
+      RC(launch_resize_cubic_f32_frames(mbase + paf_off, mrow, mpx, mframe, lh, lw, OP_N_PAF, mid_paf, mid_f, ph, pw, n,
+                                        c->stream));
+      RC(launch_resize_cubic_f32_frames(mbase + heat_off, mrow, mpx, mframe, lh, lw, OP_N_HEAT, mid_heat, mid_f, ph, pw, n,
+                                        c->stream));
     }
   }
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
