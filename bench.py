@@ -276,8 +276,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="frames per step per GPU; default 232 for the 368x368 headline, 64 for 1280x720 single "
-                         "scale (6 frame-aligned 640-px tiles per 82 x 46 map: 768 workgroups = 3 full rounds; "
-                         "981-989 -> 991-995 frames/s over 63, profiles/r03/ab_r03_c5_batch_63_64.log), 16 for --precise.  232: the 7x7 kernel's 640-pixel raster tiles, "
+                         "scale (756 7x7 workgroups, 2.95 rounds; 981-989 -> 991-995 frames/s over 63 in an "
+                         "interleaved A/B, profiles/r03/ab_r03_c5_batch_63_64.log), 16 for --precise.  232: the 7x7 kernel's 640-pixel raster tiles, "
                          "232 x 2116 / 640 = 767.05 -> 768 per branch x 2 = 1536 workgroups = six full rounds of "
                          "one per CU (114 frames left 14 CUs idle in its third round); interleaved A/B "
                          "1818-1824 / 1827-1835 / 1847-1849 frames/s at 114 / 116 / 232, "
