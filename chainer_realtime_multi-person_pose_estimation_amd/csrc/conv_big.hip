@@ -893,6 +893,8 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       census_add(npx);
       if (tl.ksplit > 1) census_add(OP_CENSUS_7X7_SPLITK);
       if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
+      if (tl.fa_tiles) census_add(OP_CENSUS_7X7_FRAME_ALIGNED);
+      if (tl.pitch == s.w + 6) census_add(OP_CENSUS_7X7_TIGHT);
       const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
       if (rc != OP_OK) return rc;
       if (tl.ksplit > 1) {

@@ -221,6 +221,10 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
     g->rec_cap = std::max(g->rec_cap, mine);
     if (g->rank == 0) g->all_cap = std::max(g->all_cap, all);
   }
+  // packing rewrites slot k's keep buffers (overflow headers, rows, maps): a waited-for gather in
+  // that slot can no longer be queried (op_comm_overflow* then report OP_ERR_STATE, never a mix of
+  // two steps' data)
+  if (g->last == k) g->last = -1;
   hipStream_t cst;
   RC(ctx_pack_records(ctx, first, n, max_persons, frame_base, frame_stride, g->d_rec[k], &cst, k));
   OP_HIP_CHECK(hipEventRecord(g->ev_packed[k], cst));

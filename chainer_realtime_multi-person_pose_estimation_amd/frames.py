@@ -335,9 +335,11 @@ class RcclGather(object):
         Collective: every rank calls it once per submit (the overflow exchange is a TCP gather)."""
         ct = self._ct
         p, nf, rb = ct.c_void_p(), ct.c_int32(), ct.c_int64()
+        # op_comm_wait dequeues the oldest slot even when it then fails (timeout, HIP error): pop the
+        # matching submit first, so this FIFO and the C slot FIFO stay in step
+        base, stride = self._sub.pop(0) if self._sub else (0, 1)
         self._lib.check(self._lib.lib().op_comm_wait(self.h, float(timeout or self.timeout), ct.byref(p),
                                                      ct.byref(nf), ct.byref(rb)), "op_comm_wait")
-        base, stride = self._sub.pop(0)
         t0 = time.perf_counter()
         own = self._own_overflow(base, stride)
         self.overflow_s += time.perf_counter() - t0

@@ -288,7 +288,10 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_3X3_R128 20    /* conv_m16r_bf16x3<4, ...> (128 channels per workgroup) */
 #define OP_CENSUS_3X3_R_POOL 21  /* conv_m16r_bf16x3<., ., ., true> (fused 2x2 max-pool) */
 #define OP_CENSUS_7X7_PLANAR 22  /* 7x7 launches on chunk-planar tensors (op_set_stage_layout) */
-#define OP_CENSUS_SLOTS 24
+#define OP_CENSUS_7X7_FRAME_ALIGNED 23  /* conv_m16 7x7 launches on frame-aligned raster tiles (no tile
+                                           crosses a frame; else batch rasters that do) */
+#define OP_CENSUS_7X7_TIGHT 24   /* conv_m16 7x7 launches with the tight halo pitch w + 6 (wide maps) */
+#define OP_CENSUS_SLOTS 32
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */
@@ -332,7 +335,8 @@ int op_comm_wait(op_comm* comm, double timeout_s, const void** records, int32_t*
  * aside on the device (op_comm_overflow_result re-runs it alone, uncapped: the result
  * op_fetch_result would have given) and a frame past max_persons kept its complete result rows
  * (copied out as they are) -- so both are exact even after later steps have run; the host ships
- * them to rank 0 (frames.py: TCP).  Valid until the next op_comm_wait. */
+ * them to rank 0 (frames.py: TCP).  Valid until the next op_comm_gather_results, which packs into
+ * that gather's slot (after it, both calls return OP_ERR_STATE until the next op_comm_wait). */
 int op_comm_overflow(op_comm* comm, op_ctx* ctx, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count);
 int op_comm_overflow_result(op_comm* comm, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,
                             op_frame_result* res);

@@ -153,6 +153,82 @@ def test_staged_u8_path_at_the_headline_batch(lib, bctx, n):
         bctx.set_batch_invariant(False)
 
 
+def test_c5_stream_batch_of_64_720p_frames(lib, bctx):
+    """C5's own bench configuration (bench.py --frame 720x1280: 64 u8 1280x720 frames per step,
+    single scale, net 656x368, maps 82x46 -> 576x320): upload -> run_staged.  The 7x7 launches run
+    NPX 10 batch-raster tiles on the 82-column maps (3772 px per frame: tiles cross frame borders
+    mid-row; conv_big.hip raster_tiling), which no single frame and no 368x368 batch reaches.
+
+    * op_conv_census: every 7x7 launch is conv_m16_bf16x3<7, 10> on batch rasters (not
+      frame-aligned), no split-K;
+    * every frame == that frame staged alone, bit for bit;
+    * frames 0, 31 (its first rows share a tile with frame 30's last: the tile starts at pixel
+      116480 = frame 30 row 40 col 40) and 63 <= 1e-3 vs the CPU oracle on the same u8 path
+      (cv2-LINEAR resize, preprocess, the reference network's forward, models/CocoPoseNet.py:132-262);
+    * with the reference-generated twenty_720p maps staged for all 64 frames (what the bench's
+      post-process reads), every frame's 576x320 post-process == the golden poses and scores bit for
+      bit (pose_detector.py:484-517)."""
+    from conftest import load_golden
+    n, H, Wd = 64, 720, 1280
+    net_w, net_h = cvresize.compute_optimal_size(H, Wd, SIDE)
+    assert (net_w, net_h) == (656, 368)
+    rng = np.random.default_rng(720)
+    frames = rng.integers(0, 256, (n, H, Wd, 3), dtype=np.uint8)
+    bctx.set_batch_invariant(True)
+    try:
+        pinned = lib.PinnedFrames(n, H, Wd)
+        try:
+            pinned.array[:] = frames
+            bctx.upload_frames(pinned.array)
+            _census_npx(lib)
+            bctx.run_staged()
+            bctx.synchronize()
+            cen = _census_npx(lib)
+            paf, heat = bctx.fetch_maps(0, n)
+        finally:
+            pinned.close()
+        print("C5 batch 64 census:", cen)
+        assert cen["npx"] == {10: 25} and cen["7x7_splitk"] == 0, cen
+        assert cen["7x7_frame_aligned"] == 0, cen  # batch rasters: tiles cross frame borders
+        assert cen["7x7_planar"] == 25, cen
+        assert paf.shape == (n, 38, 46, 82) and heat.shape == (n, 19, 46, 82)
+        W = case_weights("posenet", 0)
+        for i in (0, 31, n - 1):
+            x = cvresize.preprocess(cvresize.resize_linear_u8(frames[i], net_w, net_h))
+            opaf, oheat = F.cocoposenet_forward(W, x)
+            e = max(_max_err(paf[i], opaf[0]), _max_err(heat[i], oheat[0]))
+            print("C5 batch frame %d vs oracle: %.3g" % (i, e))
+            assert e <= TOL, (i, e)
+        for i in range(n):
+            bctx.stage_frames(frames[i:i + 1])
+            _census_npx(lib)
+            bctx.run_staged()
+            bctx.synchronize()
+            assert 10 not in _census_npx(lib)["npx"]  # the lone frame runs other tiles
+            p1, h1 = bctx.fetch_maps(0, 1)
+            assert np.array_equal(paf[i], p1[0]) and np.array_equal(heat[i], h1[0]), i
+    finally:
+        bctx.set_batch_invariant(False)
+    # the bench's post-process input: the twenty_720p maps staged for every frame of the batch
+    d = load_golden("twenty_720p")
+    assert (int(d["orig_h"]), int(d["orig_w"])) == (H, Wd) and (int(d["map_h"]), int(d["map_w"])) == (320, 576)
+    maps = np.ascontiguousarray(np.concatenate([d["paf_low"], d["heat_low"]])[None].repeat(n, axis=0))
+    bctx.stage_frames(frames)
+    bctx.stage_maps(maps)
+    bctx.use_staged_maps(True)
+    try:
+        bctx.run_staged()
+        bctx.synchronize()
+        res = bctx.fetch_results(0, n)
+    finally:
+        bctx.use_staged_maps(False)
+    assert len(res) == n
+    for i, (p, s, r) in enumerate(res):
+        assert r.map_w == 576 and r.map_h == 320 and r.n_peaks == len(d["all_peaks"]), i
+        assert np.array_equal(np.asarray(p).reshape(d["poses"].shape), d["poses"]), i
+        assert np.array_equal(s, d["scores"]), i
+
+
 def test_precise_staged_batch_of_16_equals_single_frames(lib):
     """The C4 line's batch (bench.py --precise: 16 frames of 1280x720, 4 scales): the per-scale
     batched forwards run NPX 8 / 10 tiles that one frame never reaches; every frame's averaged maps

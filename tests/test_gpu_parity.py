@@ -439,7 +439,9 @@ def test_detect_precise_vs_oracle(lib, rand_weights_small, prec):
 
 def test_staged_precise_batch_equals_per_frame(lib, rand_weights):
     """op_run_staged_precise (all staged frames batched per scale) == op_detect_precise per frame:
-    poses, scores and status identical, incl. frames whose noise maps exceed a cap / raise."""
+    poses, scores and status identical, incl. frames whose noise maps exceed the batched caps (re-run
+    uncapped) or raise the reference's IndexError (pose_detector.py:197).  Any other exception (a HIP
+    failure surfaces as RuntimeError) fails the test: it is never compared as an outcome."""
     W = {k: (w, b.copy()) for k, (w, b) in rand_weights.items()}
     for k in ("Mconv7_stage6_L1", "Mconv7_stage6_L2"):  # fewer noise peaks on the random maps
         W[k] = (W[k][0], W[k][1] - np.float32(0.3))
@@ -453,8 +455,8 @@ def test_staged_precise_batch_equals_per_frame(lib, rand_weights):
         for f in frames:
             try:
                 single.append((0,) + tuple(c.detect_precise(f)[:2]))
-            except (IndexError, RuntimeError) as e:
-                single.append((type(e).__name__,))
+            except IndexError:
+                single.append(("IndexError",))
         c.stage_frames(frames)
         c.run_staged_precise()
         for i in range(3):
@@ -462,8 +464,8 @@ def test_staged_precise_batch_equals_per_frame(lib, rand_weights):
                 p, s_, r = c.fetch_result(i)
                 got = (0, p, s_)
                 assert r.map_w == 104 and r.map_h == 72
-            except (IndexError, RuntimeError) as e:
-                got = (type(e).__name__,)
+            except IndexError:
+                got = ("IndexError",)
             assert got[0] == single[i][0]
             if got[0] == 0:
                 assert np.array_equal(got[1], single[i][1]) and np.array_equal(got[2], single[i][2])
