@@ -32,7 +32,7 @@ EXPORTED = (
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
-    "op_train_enable_layer", "op_train_step",
+    "op_train_enable_layer", "op_train_set_grad_scale", "op_train_step",
 )
 ARCH = {"facenet": 1, "handnet": 2}
 MAX_SCALES = 8
@@ -146,6 +146,7 @@ def lib():
         "op_train_get_weights": ([P, P, P, P, P], ctypes.c_int),
         "op_train_set_hyper": ([P, D, D, D, D], ctypes.c_int),
         "op_train_enable_layer": ([P, I32, I32], ctypes.c_int),
+        "op_train_set_grad_scale": ([P, I32, D], ctypes.c_int),
         "op_train_step": ([P, P, P, P, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -769,6 +770,9 @@ class TrainContext(object):
 
     def enable(self, layer_index, on=True):
         check(lib().op_train_enable_layer(self.h_, int(layer_index), int(bool(on))), "op_train_enable_layer")
+
+    def set_grad_scale(self, layer_index, scale):
+        check(lib().op_train_set_grad_scale(self.h_, int(layer_index), float(scale)), "op_train_set_grad_scale")
 
     def step(self, x, pafs_t, heatmaps_t, ignore_mask):
         n, h8, w8 = self.n, self.h // 8, self.w // 8

@@ -682,7 +682,7 @@ int op_train_create(int32_t device, int32_t n, int32_t h, int32_t w, op_train_ct
     c->cop[l] = (d.co + 63) / 64 * 64;
     c->cin_phys[l] = cv.cin_phys;
     c->dcop[l] = (cv.cin_phys + 63) / 64 * 64;
-    c->scale[l] = l < 12 ? 0.25f : 1.0f;  // GradientScaling(1/4): conv1_1 .. conv4_4_CPM
+    c->scale[l] = 1.0f;  // no hook until op_train_set_grad_scale (the reference's GradientScaling)
     c->enabled[l] = true;
     float** arrs[] = {&c->W[l], &c->gW[l], &c->mW[l], &c->vW[l]};
     for (float** a : arrs) {
@@ -794,6 +794,16 @@ int op_train_enable_layer(op_train_ctx* c, int32_t layer, int32_t enable) {
     OP_HIP_CHECK(hipMemsetAsync(c->gb[layer], 0, (size_t)d.co * 4, c->stream));
   }
   c->enabled[layer] = enable != 0;
+  return OP_OK;
+}
+
+int op_train_set_grad_scale(op_train_ctx* c, int32_t layer, double scale) {
+  TRC(tr_check(c));
+  if (layer < 0 || layer >= kNL || !(scale == scale)) {
+    set_error("op_train_set_grad_scale: bad layer or scale");
+    return OP_ERR_INVALID;
+  }
+  c->scale[layer] = (float)scale;  // grad *= scale in f32 (train_coco_pose_estimation.py:38)
   return OP_OK;
 }
 

@@ -50,10 +50,27 @@ def draw_disc(canvas, center, radius, color):
     _paint(canvas, xx * xx + yy * yy <= radius * radius, y - radius, x - radius, color)
 
 
-def draw_person_pose(orig_img, poses):
-    """pose_detector.py:520-553."""
+class Raster(object):
+    """The two OpenCV primitives draw_person_pose uses, with cv2's argument order:
+    ``line(img, pt1, pt2, color, thickness)`` and ``circle(img, center, radius, color, thickness)``
+    (thickness -1 = filled).  The default draws with the approximations above; tests pass a
+    recording subclass to compare the call sequence with the reference's own
+    (tests/golden/draw_calls.json, made by running pose_detector.py:520-553 under a recording cv2)."""
+
+    def line(self, img, pt1, pt2, color, thickness):
+        draw_line(img, pt1, pt2, color, thickness)
+
+    def circle(self, img, center, radius, color, thickness):
+        if thickness >= 0:
+            raise ValueError("draw.Raster.circle: only filled discs (thickness -1) are drawn")
+        draw_disc(img, center, radius, color)
+
+
+def draw_person_pose(orig_img, poses, raster=None):
+    """pose_detector.py:520-553 (``raster``: the cv2 stand-in, default Raster())."""
     if len(poses) == 0:
         return orig_img
+    cv = raster if raster is not None else Raster()
     canvas = orig_img.copy()
     poses_i = np.asarray(poses).round().astype("i")
     for pose in poses_i:  # limbs
@@ -63,11 +80,11 @@ def draw_person_pose(orig_img, poses):
             ind = np.array([int(j) for j in limb])
             if np.all(pose[ind][:, 2] != 0):
                 (a, b) = pose[ind][:, :2]
-                draw_line(canvas, tuple(a), tuple(b), color, 2)
+                cv.line(canvas, tuple(a), tuple(b), color, 2)
     for pose in poses_i:  # joints
         for (x, y, v), color in zip(pose, JOINT_COLORS):
             if v != 0:
-                draw_disc(canvas, (x, y), 3, color)
+                cv.circle(canvas, (x, y), 3, color, -1)
     return canvas
 
 

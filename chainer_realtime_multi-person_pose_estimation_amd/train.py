@@ -1,11 +1,14 @@
 """Training of CocoPoseNet on the MI355X path: train_coco_pose_estimation.py.
 
-``Updater`` mirrors the reference's ``Updater.update_core`` (:93-123) on one device: every
-iteration runs ``preprocess`` (:80-86, host), then forward + ``compute_loss`` (:42-77) + backward +
-``GradientScaling(1/4)`` on conv1_1 .. conv4_4_CPM (:24-38, :218-222) + ``optimizers.Adam`` (:214)
+``Updater`` mirrors the reference's ``Updater.update_core`` (:90-126) on one device: every
+iteration runs ``preprocess`` (:76-82, host), then forward + ``compute_loss`` (:41-73) + backward +
+``GradientScaling(1/4)`` on conv1_1 .. conv4_4_CPM (:25-38, :213-217) + ``optimizers.Adam`` (:210)
 in one call into the HIP library (op_train_step, exact f32).  The schedule is the reference's: the
-VGG layers conv1_1 .. conv4_2 start frozen (:225-230) and are enabled at iteration 2000 (:97-102);
-alpha 1e-4, then 1e-5 from 100k and 1e-6 from 200k iterations (:104-107).
+VGG layers conv1_1 .. conv4_2 start frozen (:219-225) and are enabled at iteration 2000 (:95-100);
+alpha 1e-4, then 1e-5 from 100k and 1e-6 from 200k iterations (:102-105).  All of it (Adam's
+hyperparameters, the hook's layers and scale, the frozen layers, the re-enable and the alpha at
+each schedule edge) is pinned to the reference's own script run under recording stubs
+(tests/golden/make_golden_train_host.py -> tests/golden/train/host_schedule.json).
 
 The COCO data pipeline (coco_data_loader.py, pycocotools, getData.sh) needs the dataset and the
 network: ``synthetic_batch`` stands in with seeded images and COCO-like maps of random skeletons
@@ -31,27 +34,65 @@ GRAD_SCALED = VGG_FROZEN + ["conv4_3_CPM", "conv4_4_CPM"]
 
 
 def preprocess(imgs):
-    """train_coco_pose_estimation.py:80-86: (n, h, w, 3) uint8 BGR -> (n, 3, h, w) f32, x/255 - 0.5."""
+    """train_coco_pose_estimation.py:76-82: (n, h, w, 3) uint8 BGR -> (n, 3, h, w) f32, x/255 - 0.5."""
     x = np.asarray(imgs).astype("f")
     x /= 255
     x -= 0.5
     return np.ascontiguousarray(x.transpose(0, 3, 1, 2))
 
 
+class GradientScaling(object):
+    """train_coco_pose_estimation.py:25-38: multiplies the gradients of ``layer_names`` by ``scale``
+    (in f32, ``grad *= scale``) before the optimizer's update.  Registered with
+    ``Updater.add_hook`` (the reference's ``optimizer.add_hook``, :213-217); on the device the scale
+    is applied inside op_train_step (op_train_set_grad_scale)."""
+
+    name = "GradientScaling"
+
+    def __init__(self, layer_names, scale):
+        self.layer_names = layer_names
+        self.scale = scale
+
+    def __call__(self, updater):
+        for layer_name in self.layer_names:
+            updater.ctx.set_grad_scale(updater.names.index(layer_name), self.scale)
+
+
+def alpha_at(iteration, alpha):
+    """update_core's learning-rate schedule (:102-105): the optimizer's alpha before the update of
+    ``iteration``, given the alpha in force before it (the reference only ever lowers it)."""
+    if 100000 <= iteration < 200000:
+        return 1e-5
+    if 200000 <= iteration:
+        return 1e-6
+    return alpha
+
+
 class Updater(object):
-    """One device, one batch shape (n, h, w).  ``update(batch)`` = Updater.update_core."""
+    """One device, one batch shape (n, h, w).  ``update(batch)`` = Updater.update_core (:90-126).
+
+    Set up like the reference's ``__main__`` (:208-225) for ``posenet``: ``optimizers.Adam(alpha=1e-4,
+    beta1=0.9, beta2=0.999, eps=1e-8)``, ``GradientScaling(conv1_1 .. conv4_4_CPM, 1/4)`` and, unless
+    resuming, conv1_1 .. conv4_2 frozen (re-enabled at iteration 2000).  ``ctx`` (tests) replaces the
+    device context: anything with set_weights / set_hyper / enable / set_grad_scale / step / get."""
 
     def __init__(self, n, h=368, w=368, model=None, device=0, alpha=1e-4, beta1=0.9, beta2=0.999, eps=1e-8,
-                 resume=False):
-        self.ctx = _lib.TrainContext(n, h, w, device)
+                 resume=False, ctx=None):
+        self.ctx = ctx if ctx is not None else _lib.TrainContext(n, h, w, device)
         self.names = [t[0] for t in self.ctx.table]
         self.iteration = 0
         self.alpha, self.beta1, self.beta2, self.eps = alpha, beta1, beta2, eps
+        self.hooks = []
         self.ctx.set_weights(model if model is not None else _weights.random_weights(0))
         self.ctx.set_hyper(alpha, beta1, beta2, eps)
+        self.add_hook(GradientScaling(GRAD_SCALED, 1 / 4))
         if not resume:
             for name in VGG_FROZEN:
                 self.disable_update(name)
+
+    def add_hook(self, hook):
+        self.hooks.append(hook)
+        hook(self)
 
     def enable_update(self, name):
         self.ctx.enable(self.names.index(name), True)
@@ -65,12 +106,8 @@ class Updater(object):
         if self.iteration == 2000:
             for name in VGG_FROZEN:
                 self.enable_update(name)
-        alpha = self.alpha
-        if 100000 <= self.iteration < 200000:
-            alpha = 1e-5
-        elif 200000 <= self.iteration:
-            alpha = 1e-6
-        self.ctx.set_hyper(alpha, self.beta1, self.beta2, self.eps)
+        self.alpha = alpha_at(self.iteration, self.alpha)
+        self.ctx.set_hyper(self.alpha, self.beta1, self.beta2, self.eps)
         imgs, pafs, heatmaps, ignore_mask = batch
         losses = self.ctx.step(preprocess(imgs), pafs, heatmaps, ignore_mask)
         self.iteration += 1

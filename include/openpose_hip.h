@@ -397,10 +397,13 @@ int op_train_get_weights(op_train_ctx* ctx, float* const* W, float* const* b, fl
 int op_train_set_hyper(op_train_ctx* ctx, double alpha, double beta1, double beta2, double eps);
 /* enable_update / disable_update of one layer (:225-230, :97-102). */
 int op_train_enable_layer(op_train_ctx* ctx, int32_t layer, int32_t enable);
+/* GradientScaling hook (train_coco_pose_estimation.py:25-38, registered at :213-217): the step
+ * multiplies this layer's W and b gradients by `scale` (f32) before Adam.  Default 1 (no hook). */
+int op_train_set_grad_scale(op_train_ctx* ctx, int32_t layer, double scale);
 /* One iteration: x = preprocess(imgs) (n, 3, h, w) f32; pafs_t (n, 38, h/8, w/8), heat_t (n, 19, h/8,
  * w/8) f32; ignore (n, h/8, w/8) u8 (1 = ignored); losses[12] = per stage (paf, heat) MSE of
- * compute_loss (:42-77).  Forward, loss, backward, GradientScaling(1/4) on conv1_1 .. conv4_4_CPM,
- * Adam on the enabled layers. */
+ * compute_loss (:42-77).  Forward, loss, backward, the per-layer gradient scales
+ * (op_train_set_grad_scale), Adam on the enabled layers. */
 int op_train_step(op_train_ctx* ctx, const float* x, const float* pafs_t, const float* heat_t, const uint8_t* ignore,
                   double* losses);
 

@@ -1,5 +1,6 @@
 """draw_person_pose (pose_detector.py:520-553): colours, skipped limbs, undetected joints."""
 import numpy as np
+import pytest
 
 from conftest import pkg_module
 
@@ -36,6 +37,48 @@ def test_undetected_joint_breaks_its_limbs():
     pose[0, 8] = (10, 40, 0)  # not detected
     out = D.draw_person_pose(img, pose)
     assert tuple(out[25, 10]) == (0, 0, 0)
+
+
+def _draw_cases():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "draw_calls.json")) as f:
+        return json.load(f)
+
+
+DRAW_CASES = _draw_cases()
+
+
+@pytest.mark.parametrize("case", sorted(DRAW_CASES))
+def test_draw_call_sequence_equals_the_reference(case):
+    """The reference's own draw_person_pose (pose_detector.py:520-553), run unmodified under a
+    recording cv2 stub (tests/golden/make_golden_draw.py), made exactly these cv2.line /
+    cv2.circle calls -- same order, endpoints, colours, thickness, radius, on a copy of the input;
+    the package's draw_person_pose must make the identical sequence (the rasteriser behind the
+    calls stays unpinned: OpenCV is absent)."""
+    D = pkg_module("draw")
+    c = DRAW_CASES[case]
+    img = np.zeros((c["h"], c["w"], 3), np.uint8)
+    calls = []
+
+    class Recorder(D.Raster):
+        def line(self, canvas, pt1, pt2, color, thickness):
+            calls.append({"op": "line", "pt1": [int(v) for v in pt1], "pt2": [int(v) for v in pt2],
+                          "color": [float(v) for v in color], "thickness": int(thickness), "canvas": canvas})
+            super().line(canvas, pt1, pt2, color, thickness)
+
+        def circle(self, canvas, center, radius, color, thickness):
+            calls.append({"op": "circle", "center": [int(v) for v in center], "radius": int(radius),
+                          "color": [float(v) for v in color], "thickness": int(thickness), "canvas": canvas})
+            super().circle(canvas, center, radius, color, thickness)
+
+    res = D.draw_person_pose(img, np.asarray(c["poses"], np.float64).reshape(-1, 18, 3), raster=Recorder())
+    assert (res is img) == c["returns_input"]
+    for k in calls:
+        k["canvas"] = "returned" if k["canvas"] is res else ("input" if k["canvas"] is img else "other")
+    assert calls == c["calls"]
+    if not c["returns_input"]:
+        assert img.sum() == 0  # the input is never drawn on
 
 
 def test_read_bgr_drops_alpha_like_imread_color():

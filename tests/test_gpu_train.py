@@ -60,6 +60,13 @@ def torch_step(W, x, pafs_t, heat_t, ignore):
     return np.array(losses), {k: (w.grad.numpy(), b.grad.numpy()) for k, (w, b) in P.items()}
 
 
+def _hook_multipliers():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "train", "host_schedule.json")) as f:
+        return json.load(f)["hooks"][0]["multiplier_by_layer"]
+
+
 def adam_ref(p, g, scale, t, alpha=1e-4, b1=0.9, b2=0.999, eps=1e-8):
     """Chainer AdamRule on fresh state after t identical-gradient steps is not what we test; one step."""
     g = (g * np.float32(scale)).astype(np.float32)
@@ -89,6 +96,12 @@ def test_train_step_vs_torch_float64(frozen):
         ctx.set_weights(W0)
         ctx.set_hyper(1e-4)
         names = [t[0] for t in ctx.table]
+        # the reference's GradientScaling hook, as its own __call__ applied it per layer
+        # (tests/golden/train/host_schedule.json, make_golden_train_host.py)
+        mult = _hook_multipliers()
+        for nm, sc in mult.items():
+            if sc != 1.0:
+                ctx.set_grad_scale(names.index(nm), sc)
         vgg = pkg_module("train").VGG_FROZEN
         if frozen:
             for nm in vgg:
@@ -100,7 +113,6 @@ def test_train_step_vs_torch_float64(frozen):
         ctx.close()
     ref_losses, ref_grads = torch_step(W0, x, pt, ht, ig)
     np.testing.assert_allclose(losses, ref_losses, rtol=2e-5)
-    scaled = pkg_module("train").GRAD_SCALED
     worst = 0.0
     for nm in names:
         gW, gb = grads[nm]
@@ -114,8 +126,8 @@ def test_train_step_vs_torch_float64(frozen):
         errb = np.abs(gb - rb).max() / max(np.abs(rb).max(), 1e-30)
         worst = max(worst, errW, errb)
         assert errW <= 2e-3 and errb <= 2e-3, (nm, errW, errb)
-        # the Adam step on the device's own gradients (GradientScaling 1/4 on the VGG + CPM layers)
-        sc = 0.25 if nm in scaled else 1.0
+        # the Adam step on the device's own gradients times the reference hook's multiplier
+        sc = mult[nm]
         np.testing.assert_allclose(W1[nm][0], adam_ref(W0[nm][0], gW, sc, 1), rtol=0, atol=2e-7)
         np.testing.assert_allclose(W1[nm][1], adam_ref(W0[nm][1], gb, sc, 1), rtol=0, atol=2e-7)
     print("train step: max relative gradient error vs float64 = %.3g" % worst)
