@@ -269,6 +269,73 @@ def measure(run, ctx, transport, steps, warmup, prof_7x7):
     return elapsed, prof
 
 
+def batch1_line(L, ctx, low, FH, FW, steps=60, warmup=10):
+    """Single-image latency (BASELINE config 2 "single 368x368 frame"; pose_detector.py:484-517 is a
+    one-image call): per step ONE pinned u8 frame is uploaded, run through the whole path (resize +
+    normalise, 92 convs, post-process on the staged 6-person maps) and its poses fetched to the host,
+    synchronously -- eager launches and a replayed hipGraph.  ms_per_frame = wall time per call;
+    the eager run also times the 7x7 launches with HIP events (frac of the 833 TF/s bf16x3 peak)
+    and, over a few extra calls, every kernel class."""
+    pinned = L.PinnedFrames(1, FH, FW)
+    rng = np.random.default_rng(99)
+    pinned.array[...] = rng.integers(0, 256, (1, FH, FW, 3), dtype=np.uint8)
+    ctx.stage_frames(np.zeros((1, FH, FW, 3), np.uint8))
+    if low is not None:
+        ctx.stage_maps(np.ascontiguousarray(low[None]))
+        ctx.use_staged_maps(True)
+    out = {}
+    try:
+        for graph in (0, 1):
+            def call():
+                ctx.upload_frames(pinned.array)
+                ctx.run_staged(graph=bool(graph))
+                ctx.synchronize()
+                return ctx.fetch_results(0, 1)
+            for _ in range(warmup):
+                call()
+            ctx.profile_classes(["conv7x7"])
+            ctx.profile(not graph)
+            ctx.profile_reset()
+            times = []
+            for _ in range(steps):
+                t0 = time.perf_counter()
+                r = call()
+                times.append(time.perf_counter() - t0)
+            prof = ctx.profile_read()
+            ctx.profile(False)
+            key = "graph" if graph else "eager"
+            med = statistics.median(times)
+            line = {"ms_per_frame_median": round(med * 1e3, 4), "ms_per_frame_min": round(min(times) * 1e3, 4),
+                    "frames_per_s": round(1.0 / med, 2), "persons": int(r[0][2].n_persons)}
+            ms7, n7, fl7, _ = prof["conv7x7"]
+            if not graph and n7 and ms7 > 0:
+                line["conv7x7_ms"] = round(ms7 / steps, 4)
+                line["conv7x7_frac_of_833"] = round(fl7 / (ms7 * 1e-3) / 1e12 / (BF16_DENSE_PEAK_TFLOPS / 3.0), 4)
+            out[key] = line
+        ctx.profile_classes(list(ctx.PROFILE_CLASSES))
+        ctx.profile(True)
+        ctx.profile_reset()
+        for _ in range(10):
+            ctx.upload_frames(pinned.array)
+            ctx.run_staged()
+            ctx.synchronize()
+        pall = ctx.profile_read()
+        ctx.profile(False)
+        out["stage_ms_per_frame"] = {k: round(v[0] / 10, 4) for k, v in pall.items() if v[1]}
+        L.conv_census(reset=True)
+        ctx.upload_frames(pinned.array)
+        ctx.run_staged()
+        ctx.synchronize()
+        cen = L.conv_census(reset=True)
+        out["conv7x7_tiles"] = {"npx": cen["npx"], "splitk_launches": cen["7x7_splitk"]}
+        out["note"] = ("one %dx%d frame per synchronous call: upload, run_staged, fetch_results; median of %d "
+                       "calls after %d warm-up" % (FW, FH, steps, warmup))
+    finally:
+        ctx.use_staged_maps(False)
+        pinned.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -474,6 +541,8 @@ def main():
                             "stage_ms_per_step": {k: round(v[0] / 3, 3) for k, v in pall.items()},
                             "stage_ms_note": "HIP-event sums per kernel class over 3 untimed profiled steps"}
         ctx.set_precision(args.precision)
+        # single-image latency (BASELINE config 2 names one 368x368 frame): last, it re-stages
+        variants["batch1"] = batch1_line(L, ctx, low, FH, FW)
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         frames = run.pool[0].array[:4].copy()
