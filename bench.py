@@ -100,7 +100,9 @@ def cpu_baseline(frames, low_maps, n_frames):
             "sample": "median of %d frames after 1 warm-up (%.2f s/frame, %.1f s total): oracle forward "
                       "(im2col + np.tensordot sgemm, 368x368) + NumPy/SciPy post-process restatement "
                       "(oracle/postproc_np.py) on the 6-person maps" % (n_frames, med, sum(times)),
-            "blas": vendor, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "nproc": os.cpu_count()}
+            "blas": vendor, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "nproc": os.cpu_count(),
+            "cores_note": "BLAS threads = OMP_NUM_THREADS, which the GPU box sets to the host-CPU share it "
+                          "allots one GPU (16); nproc counts every CPU of the shared machine"}
 
 
 KERNEL_7X7 = {0: "conv_bf16x3<7", 1: "conv7_halo_bf16x3", 2: "conv7_halo_bf16x3", 3: "conv_halo_bf16x3<7",
@@ -484,7 +486,10 @@ def main():
         "gflop_per_frame": round((sum(L.forward_flops(*precise_net(FH, FW, sc)) for sc in PARAMS_SCALES)
                                   if args.precise else L.forward_flops(net_h, net_w)) / 1e9, 2),
         "stage_ms_per_step": stage_ms,
-        "stage_ms_note": "HIP-event sums per kernel class over %d untimed profiled steps" % n_extra,
+        "stage_ms_sum": round(sum(stage_ms.values()), 3),
+        "stage_ms_note": "HIP-event sums per kernel class over %d untimed profiled steps (every kernel the "
+                         "step launches is in a class; the sum falls short of ms_per_step by the gaps "
+                         "between kernels)" % n_extra,
         "roofline": roofline,
     }
     if not args.no_variants and world == 1:

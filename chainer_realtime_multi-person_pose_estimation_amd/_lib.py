@@ -545,7 +545,7 @@ class Context(object):
         return a.value, b.value, t.value
 
     # ---- per-kernel-class event timing ----
-    PROFILE_CLASSES = ("conv7x7", "conv3x3", "conv1x1", "postprocess")
+    PROFILE_CLASSES = ("conv7x7", "conv3x3", "conv1x1", "postprocess", "input", "map_resize", "other")
 
     def profile(self, enable=True):
         check(lib().op_profile_enable(self.h, 1 if enable else 0), "op_profile_enable")

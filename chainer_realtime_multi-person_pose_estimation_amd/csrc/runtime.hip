@@ -335,7 +335,7 @@ struct op_ctx {
   // per-class launch profiling
   bool prof = false;
   int splitk = 1;  // op_set_batch_invariant(0): small 7x7 launches may split K
-  int prof_mask = 0xF;  // kernel classes timed while prof (op_profile_classes)
+  int prof_mask = 0x7F;  // kernel classes timed while prof (op_profile_classes)
   // set by the forward around launches it issues back to back (the 7x7 Mconv1..Mconv5 of a stage):
   // a profiled launch then extends the previous pair of its class instead of adding an event pair
   // (an event record between two kernels costs ~10 us of stream idle time on this runtime)
@@ -343,8 +343,8 @@ struct op_ctx {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<op::ProfPair> pending;
-  double prof_ms[4] = {0, 0, 0, 0}, prof_flops[4] = {0, 0, 0, 0}, prof_bytes[4] = {0, 0, 0, 0};
-  int64_t prof_n[4] = {0, 0, 0, 0};
+  double prof_ms[OP_PROFILE_CLASSES] = {}, prof_flops[OP_PROFILE_CLASSES] = {}, prof_bytes[OP_PROFILE_CLASSES] = {};
+  int64_t prof_n[OP_PROFILE_CLASSES] = {};
   // graph
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -612,6 +612,8 @@ static int profiled(op_ctx* c, int cls, double flops, double bytes, Fn fn) {
 }
 
 static int conv_class(int ks) { return ks == 7 ? 0 : (ks == 3 ? 1 : 2); }
+// the other op_profile_read classes (openpose_hip.h)
+constexpr int kProfPost = 3, kProfInput = 4, kProfMapResize = 5, kProfOther = 6;
 
 // algorithmic work of one conv group: 2*Ci*Co*k*k*N*H*W FLOPs; bytes = input + output + weights (fp32)
 static void conv_work(const op_ctx* c, const Act& out, const PackedConv& pc, double* flops, double* bytes) {
@@ -798,8 +800,10 @@ static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
 }
 
 static int pool(op_ctx* c, const Act& in, const Act& out, int ch) {
-  if (c->split) return launch_maxpool2_split(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
-  return launch_maxpool2(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
+  return profiled(c, kProfOther, 0.0, 0.0, [&] {
+    if (c->split) return launch_maxpool2_split(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
+    return launch_maxpool2(in.p, in.pad, out.p, out.pad, c->gn, in.h, in.w, ch, c->stream);
+  });
 }
 
 // frames != nullptr (split path): conv1_1 reads the uint8 frames directly (fused input kernel).
@@ -862,8 +866,10 @@ static int run_forward(op_ctx* c, const uint8_t* frames = nullptr, int64_t frame
   const bool planar = c->split && (c->conv_algo == 4 || c->conv_algo == 5) && c->stage_planar && head_fused_on() &&
                       conv_m16_takes(c->gn, sh8, sw8, 1, 256) && conv_m16_takes(c->gn, sh8, sw8, 2, 128);
   if (planar)
-    RC(launch_split_to_planar(B[B_CAT].p, B[B_CATP].p, c->gn, sh8, sw8, B[B_CAT].pad, B[B_CAT].cs, 128 / 16,
-                              c->stream));
+    RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
+      return launch_split_to_planar(B[B_CAT].p, B[B_CATP].p, c->gn, sh8, sw8, B[B_CAT].pad, B[B_CAT].cs, 128 / 16,
+                                    c->stream);
+    }));
   const Act& catm = planar ? B[B_CATP] : B[B_CAT];  // stage maps + Mconv1 input
   // stage 1 (CocoPoseNet.py:153-165)
   const Act& cat = B[B_CAT];
@@ -1859,8 +1865,10 @@ static int enqueue_staged(op_ctx* c, bool timing) {
   if (c->split) {  // the network input is resampled inside the conv1_1 kernel
     RC(run_forward(c, c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_h, c->st_w));
   } else {
-    RC(launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h, c->st_w,
-                         in_h, in_w, c->buf[B_X0].p, c->stream));
+    RC(profiled(c, kProfInput, 0.0, 0.0, [&] {
+      return launch_preprocess(c->d_frames, (int64_t)c->st_h * c->st_w * 3, (int64_t)c->st_w * 3, c->st_n, c->st_h,
+                               c->st_w, in_h, in_w, c->buf[B_X0].p, c->stream);
+    }));
     RC(run_forward(c));
   }
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[1], c->stream));
@@ -1886,7 +1894,7 @@ static int enqueue_staged(op_ctx* c, bool timing) {
   const double mp = (double)c->st_n * map_h * map_w;
   const double pbytes = 4.0 * ((double)c->st_n * 57 * lh * lw + 18 * mp + 2 * 2 * 18 * mp + 18 * mp);
   post_record(c, 1, &src, nullptr, 0, s);
-  RC(profiled(c, 3, 0.0, pbytes, [&] { return launch_post_maps(src, s, c->pb, c->stream); }));
+  RC(profiled(c, kProfPost, 0.0, pbytes, [&] { return launch_post_maps(src, s, c->pb, c->stream); }));
   if (timing) OP_HIP_CHECK(hipEventRecord(c->ev[2], c->stream));
   c->timed = timing;
   return OP_OK;
@@ -2373,9 +2381,12 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     }
     rows_cnt = k.d_rows_cnt;
   }
-  hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
-                     frame_stride, (char*)dst, record_bytes(max_persons), rows_cnt);
-  OP_AFTER_LAUNCH("pack_records", c->stream);
+  RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
+    hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
+                       frame_stride, (char*)dst, record_bytes(max_persons), rows_cnt);
+    OP_AFTER_LAUNCH("pack_records", c->stream);
+    return OP_OK;
+  }));
   if (keep_slot >= 0) {
     KeepSlot& k = c->keep[keep_slot];
     const PostRecord& r = c->post_rec;
@@ -2399,9 +2410,12 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       OP_HIP_CHECK(hipHostMalloc((void**)&k.h_hdr, hb, hipHostMallocDefault));
       k.hdr_cap = hb;
     }
-    hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                       k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt);
-    OP_AFTER_LAUNCH("keep_overflow", c->stream);
+    RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
+      hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
+                         k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt);
+      OP_AFTER_LAUNCH("keep_overflow", c->stream);
+      return OP_OK;
+    }));
     OP_HIP_CHECK(hipMemcpyAsync(k.h_hdr, k.d_hdr, hb, hipMemcpyDeviceToHost, c->stream));
     k.rec = r;
     k.rec.s.n = n;
@@ -2639,9 +2653,12 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
     const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
     RC(ensure_geometry(c, n, ph, pw));
     const Act& x0 = c->buf[B_X0];
-    for (int f = 0; f < n; ++f)
-      RC(launch_preprocess_cubic(c->d_frames + f * fbytes, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split,
-                                 x0.p + (size_t)f * x0.frame_floats(), c->stream));
+    RC(profiled(c, kProfInput, 0.0, 0.0, [&] {
+      for (int f = 0; f < n; ++f)
+        RC(launch_preprocess_cubic(c->d_frames + f * fbytes, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split,
+                                   x0.p + (size_t)f * x0.frame_floats(), c->stream));
+      return OP_OK;
+    }));
     RC(run_forward(c));
     // last-stage maps (lh, lw, cs) with the PAF / heat channels at paf_off / heat_off
     const int lh = ph / 8, lw = pw / 8;
@@ -2673,10 +2690,12 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       const int64_t mid_f = pp * (OP_N_PAF + OP_N_HEAT);
       float* mid_paf = c->d_pmid + mid_off[k];
       float* mid_heat = mid_paf + (size_t)pp * OP_N_PAF;
-      RC(launch_resize_cubic_f32_frames(mbase + paf_off, mrow, mpx, mframe, lh, lw, OP_N_PAF, mid_paf, mid_f, ph, pw, n,
-                                        c->stream));
-      RC(launch_resize_cubic_f32_frames(mbase + heat_off, mrow, mpx, mframe, lh, lw, OP_N_HEAT, mid_heat, mid_f, ph, pw, n,
-                                        c->stream));
+      RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+        RC(launch_resize_cubic_f32_frames(mbase + paf_off, mrow, mpx, mframe, lh, lw, OP_N_PAF, mid_paf, mid_f, ph, pw,
+                                          n, c->stream));
+        return launch_resize_cubic_f32_frames(mbase + heat_off, mrow, mpx, mframe, lh, lw, OP_N_HEAT, mid_heat, mid_f, ph,
+                                              pw, n, c->stream);
+      }));
     }
   }
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
@@ -2694,7 +2713,9 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       a.scx[k] = 1.0 / ((double)w / (double)rws[k]);  // cv_cubic_scale (cvcubic.hpp): OpenCV's f64 inverse scale
       a.scy[k] = 1.0 / ((double)h / (double)rhs[k]);
     }
-    RC(launch_resize_cubic_f32_planar_mean(a, c->d_psum + f * fplanes, h, w, OP_N_PAF, OP_N_HEAT, c->stream));
+    RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+      return launch_resize_cubic_f32_planar_mean(a, c->d_psum + f * fplanes, h, w, OP_N_PAF, OP_N_HEAT, c->stream);
+    }));
   }
   // :474-482 post-process at the original resolution: img_len = orig_w, no rescale.  With staged
   // full-resolution maps (op_stage_maps at the frame size + op_use_staged_maps) the post-process
@@ -2712,9 +2733,11 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   post_shape(c, s, n, h, w, h, w, (double)w, 1.0, 1.0);
   post_record(c, 2, nullptr, post_maps, fplanes, s);
   const float* sum_heat0 = post_maps + (size_t)OP_N_PAF * h * w;
-  RC(launch_peaks_from_full(sum_heat0, OP_N_JOINTS, h, w, s, c->pb, c->stream, fplanes));
-  RC(launch_connections_full(post_maps, h, w, s, c->pb, c->stream, fplanes));
-  RC(launch_grouping(s, c->pb, c->stream));
+  RC(profiled(c, kProfPost, 0.0, 0.0, [&] {
+    RC(launch_peaks_from_full(sum_heat0, OP_N_JOINTS, h, w, s, c->pb, c->stream, fplanes));
+    RC(launch_connections_full(post_maps, h, w, s, c->pb, c->stream, fplanes));
+    return launch_grouping(s, c->pb, c->stream);
+  }));
   *net_w = pws[ns - 1];
   *net_h = phs[ns - 1];
   return OP_OK;
@@ -2866,7 +2889,7 @@ int op_profile_enable(op_ctx* c, int32_t enable) {
 int op_profile_classes(op_ctx* c, int32_t mask) {
   using namespace op;
   RC(check_ctx(c, false));
-  c->prof_mask = mask & 0xF;
+  c->prof_mask = mask & ((1 << OP_PROFILE_CLASSES) - 1);
   return OP_OK;
 }
 
@@ -2876,7 +2899,7 @@ int op_profile_reset(op_ctx* c) {
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
   c->pending.clear();
   c->ev_used = 0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < OP_PROFILE_CLASSES; ++i) {
     c->prof_ms[i] = c->prof_flops[i] = c->prof_bytes[i] = 0.0;
     c->prof_n[i] = 0;
   }
@@ -2886,8 +2909,8 @@ int op_profile_reset(op_ctx* c) {
 int op_profile_read(op_ctx* c, int32_t cls, double* ms, int64_t* launches, double* flops, double* bytes) {
   using namespace op;
   RC(check_ctx(c, false));
-  if (cls < 0 || cls > 3) {
-    set_error("profile class must be 0..3");
+  if (cls < 0 || cls >= OP_PROFILE_CLASSES) {
+    set_error("profile class out of range (OP_PROFILE_CLASSES)");
     return OP_ERR_INVALID;
   }
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));

@@ -261,13 +261,17 @@ int op_fetch_maps(op_ctx* ctx, int32_t first, int32_t n, float* pafs, float* hea
 int op_last_timing(op_ctx* ctx, double* conv_ms, double* post_ms, double* total_ms);
 /* Per-kernel-class HIP-event timing of the launches enqueued by op_run_staged while enabled
  * (event pairs on the context stream around every launch of the class).  Classes:
- * 0 = 7x7 stage convs (the dominant kernel), 1 = 3x3 convs, 2 = 1x1 convs, 3 = post-process.
- * op_profile_read resolves pending pairs (after op_synchronize) and returns the totals since the
+ * 0 = 7x7 stage convs (the dominant kernel), 1 = 3x3 convs, 2 = 1x1 convs, 3 = post-process
+ * (peaks, line integrals, greedy, grouping; single scale and detect_precise's full resolution),
+ * 4 = frame input (resize + pad + normalise kernels not fused into a conv), 5 = map resizes
+ * (detect_precise's cubic resizes of the last-stage maps and their scale mean), 6 = other (pools,
+ * layout copies, result packing).  op_profile_read resolves pending pairs (after op_synchronize) and returns the totals since the
  * last reset: summed ms, launch count, algorithmic FLOPs and algorithmic HBM bytes. */
 int op_profile_enable(op_ctx* ctx, int32_t enable);
 int op_profile_read(op_ctx* ctx, int32_t cls, double* ms, int64_t* launches, double* flops, double* bytes);
 int op_profile_reset(op_ctx* ctx);
-/* Which classes op_profile_enable times (bit c = class c; default 0xF = all). */
+/* Which classes op_profile_enable times (bit c = class c; default 0x7F = all). */
+#define OP_PROFILE_CLASSES 7
 int op_profile_classes(op_ctx* ctx, int32_t mask);
 
 /* Launch census of the bf16x3 conv kernels (process-wide, all contexts; counted on the host when a
