@@ -212,6 +212,29 @@ struct CubicMeanArgs {
 };
 int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int32_t dh, int32_t dw, int32_t npaf,
                                         int32_t nheat, hipStream_t st);
+// detect_precise's two map resizes per scale fused (round 4): the padded-size maps are never
+// written; see precise.hip resize_cubic_fused_mean.  low[k]: scale k's last-stage maps, planar
+// [frame][npaf + nheat][lh][lw] f32 (launch_maps_planar).
+struct CubicFusedArgs {
+  int ns;
+  const float* low[OP_MAX_SCALES];
+  int64_t lframe[OP_MAX_SCALES];                         // floats per frame of low[k]
+  int lh[OP_MAX_SCALES], lw[OP_MAX_SCALES];              // last-stage map size
+  int pw[OP_MAX_SCALES];                                 // first resize's width (padded input width)
+  int rh[OP_MAX_SCALES], rw[OP_MAX_SCALES];              // crop = second resize's source size
+  double s1x[OP_MAX_SCALES], s1y[OP_MAX_SCALES];         // first resize: cv_cubic_scale(pw, lw), (ph, lh)
+  double s2x[OP_MAX_SCALES], s2y[OP_MAX_SCALES];         // second: cv_cubic_scale(w, rw), (h, rh)
+  int rx_cap, ry_cap, lr_cap;                            // LDS extents (host bounds)
+};
+// false (and nothing launched) when a scale's tile extents exceed the kernel's LDS budget: the
+// caller then runs the two-pass path
+size_t cubic_fused_lds(CubicFusedArgs& a);  // sets a's extents; 0 = over the kernel's LDS budget
+int launch_resize_cubic_fused_mean(CubicFusedArgs a, float* dst, int32_t n, int32_t dh, int32_t dw, int32_t npaf,
+                                   int32_t nheat, hipStream_t st, bool* taken);
+// (frames, lh, lw, cn) maps at src (row stride sstride, pixel stride pstride, frame stride fstride
+// floats) -> planar dst [frame][dst_c0 + c][lh][lw] with dst_nch channels per frame
+int launch_maps_planar(const float* src, int64_t sstride, int32_t pstride, int64_t fstride, int32_t lh, int32_t lw,
+                       int32_t cn, float* dst, int32_t dst_c0, int32_t dst_nch, int32_t n, hipStream_t st);
 int launch_resize_cubic_f32_planar(const float* src, int64_t cstride, int64_t sstride, int32_t sh, int32_t sw,
                                    int32_t cn, float* dst, int32_t dh, int32_t dw, int32_t mode, float div,
                                    hipStream_t st);

@@ -310,6 +310,246 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
   return OP_OK;
 }
 
+// Last-stage maps -> planar [frame][dst_c0 + c][lh][lw] (the fused resize's input: each scale's maps
+// copied out of its activation arena, ~6 MB per 1280x720 frame over the four scales).
+__global__ __launch_bounds__(256) void maps_planar(const float* __restrict__ src, int64_t sstride, int pstride,
+                                                   int64_t fstride, int lh, int lw, int cn, float* __restrict__ dst,
+                                                   int dst_c0, int dst_nch, int n) {
+  const int64_t plane = (int64_t)lh * lw;
+  const int64_t total = (int64_t)n * cn * plane;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t p = i % plane;
+  const int c = (int)((i / plane) % cn);
+  const int f = (int)(i / (plane * cn));
+  const int y = (int)(p / lw), x = (int)(p - (int64_t)y * lw);
+  dst[((int64_t)f * dst_nch + dst_c0 + c) * plane + p] = src[(int64_t)f * fstride + (int64_t)y * sstride +
+                                                             (int64_t)x * pstride + c];
+}
+
+int launch_maps_planar(const float* src, int64_t sstride, int32_t pstride, int64_t fstride, int32_t lh, int32_t lw,
+                       int32_t cn, float* dst, int32_t dst_c0, int32_t dst_nch, int32_t n, hipStream_t st) {
+  const int64_t total = (int64_t)n * cn * lh * lw;
+  hipLaunchKernelGGL(maps_planar, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, sstride, pstride,
+                     fstride, lh, lw, cn, dst, dst_c0, dst_nch, n);
+  OP_AFTER_LAUNCH("maps_planar", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// Both map resizes of every scale (pose_detector.py:461-467) and the scale mean (:469-470) in one
+// pass (round 4), without the padded-size maps in HBM.  cv2.resize(map, (pw, ph), CUBIC), the crop
+// [:rh, :rw] and cv2.resize(crop, (w, h), CUBIC) of a channel are a chain of separable 4-tap
+// filters; a block makes, for a TY x 256 tile of the output and one channel at a time, exactly the
+// crop elements that tile's second resize reads, in LDS:
+//   a. first resize, horizontal sums of the low-res rows those crop rows need   (H1)
+//   b. first resize, vertical sums -> the crop elements                          (I)
+//   c. second resize, horizontal sums over the crop rows, each thread its column (H2, own column)
+//   d. second resize, vertical sums of the thread's column -> the output rows,
+//      summed over the scales in scale order, divided by the scale count once.
+// Every element's f32 operations and their order are those of resize_cubic_f32_up (the first
+// resize, incl. its SIMD-body / scalar-tail orders over pw x cn) and resize_cubic_f32_planar_mean
+// (the second resize and the mean), so the averaged maps are BIT-IDENTICAL to the two-pass path
+// (tests/test_gpu_precise_full.py); HBM sees the low-res maps and the averaged output only: per
+// 1280x720 frame ~1.04 GB of padded-size map writes and reads become 210 MB of output writes.
+// kFusedTY = TY output rows per block: 16, or 8 where the scales' crops are large against the
+// output (second-resize ratios over ~1.1) and 16 rows' extents would not fit the LDS budget.
+constexpr int kFusedTX = 256, kFusedG = 8;
+template <int kFusedTY>
+__global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a, float* __restrict__ dst, int dh,
+                                                               int dw, int npaf, int nheat) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nch = npaf + nheat;
+  const int ngroups = (nch + kFusedG - 1) / kFusedG;
+  const int f = blockIdx.z / ngroups, c0 = (blockIdx.z - f * ngroups) * kFusedG;
+  const int x0 = blockIdx.x * kFusedTX, y0 = blockIdx.y * kFusedTY;
+  const int tid = threadIdx.x, x = x0 + tid;
+  const int xl = min(x0 + kFusedTX - 1, dw - 1), yl = min(y0 + kFusedTY - 1, dh - 1);
+  const int ns = a.ns, rxc = a.rx_cap, ryc = a.ry_cap;
+  CubicTap* t1x = (CubicTap*)lds;                  // [ns][rx_cap]
+  CubicTap* t1y = t1x + ns * rxc;                  // [ns][ry_cap]
+  CubicTap* t2y = t1y + ns * ryc;                  // [ns][TY]
+  float* H1 = (float*)(t2y + ns * kFusedTY);       // [lr_cap][rx_cap]
+  float* I = H1 + a.lr_cap * rxc;                  // [ry_cap][rx_cap]
+  float* H2 = I + ryc * rxc;                       // [ry_cap][TX]
+  // per scale: the crop columns / rows the tile reads and the low-res rows those rows read (in LDS:
+  // the scale loop below is not unrolled, so per-scale register arrays would go to scratch)
+  __shared__ int rq[6][OP_MAX_SCALES];  // qx0, nqx, qy0, nqy, l0, nl
+  for (int k = 0; k < ns; ++k) {
+    const int rw = a.rw[k], rh = a.rh[k];
+    const int qx0 = clampc(cv_cubic_tap_s(x0, a.s2x[k]).s - 1, 0, rw - 1);
+    const int qy0 = clampc(cv_cubic_tap_s(y0, a.s2y[k]).s - 1, 0, rh - 1);
+    const int nqy = clampc(cv_cubic_tap_s(yl, a.s2y[k]).s + 2, 0, rh - 1) - qy0 + 1;
+    const int nqx = clampc(cv_cubic_tap_s(xl, a.s2x[k]).s + 2, 0, rw - 1) - qx0 + 1;
+    const int l0 = clampc(cv_cubic_tap_s(qy0, a.s1y[k]).s - 1, 0, a.lh[k] - 1);
+    if (tid == 0) {
+      rq[0][k] = qx0;
+      rq[1][k] = nqx;
+      rq[2][k] = qy0;
+      rq[3][k] = nqy;
+      rq[4][k] = l0;
+      rq[5][k] = clampc(cv_cubic_tap_s(qy0 + nqy - 1, a.s1y[k]).s + 2, 0, a.lh[k] - 1) - l0 + 1;
+    }
+    for (int i = tid; i < nqx; i += 256) t1x[k * rxc + i] = cv_cubic_tap_s(qx0 + i, a.s1x[k]);
+    for (int i = tid; i < nqy; i += 256) t1y[k * ryc + i] = cv_cubic_tap_s(qy0 + i, a.s1y[k]);
+    if (tid < kFusedTY) t2y[k * kFusedTY + tid] = cv_cubic_tap_s(min(y0 + tid, dh - 1), a.s2y[k]);
+  }
+  __syncthreads();
+  const int64_t plane = (int64_t)dh * dw;
+  for (int g = 0; g < kFusedG; ++g) {
+    const int c = c0 + g;
+    if (c >= nch) break;
+    const bool paf = c < npaf;
+    const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+    float sum[kFusedTY];
+    for (int k = 0; k < ns; ++k) {
+      const int lw = a.lw[k], lh = a.lh[k], rw = a.rw[k], rh = a.rh[k];
+      const int qx0 = rq[0][k], NX = rq[1][k], qy0 = rq[2][k], NY = rq[3][k], l0 = rq[4][k], NL = rq[5][k];
+      if (NX > rxc || NY > ryc || NL > a.lr_cap) {  // never (host bounds); loud if they were wrong
+        if (x < dw)
+          for (int yy = 0; yy < kFusedTY; ++yy) sum[yy] = __builtin_nanf("");
+        continue;
+      }
+      const float* src = a.low[k] + (int64_t)f * a.lframe[k] + (int64_t)c * lh * lw;
+      // a. H1[l][i]: low-res row l0 + l, crop column qx0 + i (resize_cubic_f32_up's horizontal sum)
+      for (int j = tid; j < NL * NX; j += 256) {
+        const int l = j / NX, i = j - l * NX;
+        const CubicTap t = t1x[k * rxc + i];
+        const float* row = src + (int64_t)(l0 + l) * lw;
+        float h = __fmul_rn(row[clampc(t.s - 1, 0, lw - 1)], t.c[0]);
+        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s, 0, lw - 1)], t.c[1]));
+        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s + 1, 0, lw - 1)], t.c[2]));
+        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s + 2, 0, lw - 1)], t.c[3]));
+        H1[l * rxc + i] = h;
+      }
+      __syncthreads();  // also: every thread's step c of the previous scale / channel has read I
+      // b. I[r][i]: the first resize's output at (qy0 + r, qx0 + i), its vertical order over pw x cn
+      const int simd1 = a.pw[k] * cn / 4 * 4;
+      for (int j = tid; j < NY * NX; j += 256) {
+        const int r = j / NX, i = j - r * NX;
+        const CubicTap t = t1y[k * ryc + r];
+        const float h0 = H1[(clampc(t.s - 1, 0, lh - 1) - l0) * rxc + i];
+        const float h1 = H1[(clampc(t.s, 0, lh - 1) - l0) * rxc + i];
+        const float h2 = H1[(clampc(t.s + 1, 0, lh - 1) - l0) * rxc + i];
+        const float h3 = H1[(clampc(t.s + 2, 0, lh - 1) - l0) * rxc + i];
+        float v;
+        if ((qx0 + i) * cn + ce < simd1) {
+          const float t3 = __fmul_rn(h3, t.c[3]);
+          const float t2 = __fadd_rn(__fmul_rn(h2, t.c[2]), t3);
+          const float t1 = __fadd_rn(__fmul_rn(h1, t.c[1]), t2);
+          v = __fadd_rn(__fmul_rn(h0, t.c[0]), t1);
+        } else {
+          v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, t.c[0]), __fmul_rn(h1, t.c[1])), __fmul_rn(h2, t.c[2])),
+                        __fmul_rn(h3, t.c[3]));
+        }
+        I[r * rxc + i] = v;
+      }
+      __syncthreads();
+      // c + d: this thread's output column (no barrier: H2's column is the thread's own)
+      if (x < dw) {
+        const CubicTap t = cv_cubic_tap_s(x, a.s2x[k]);
+        int col[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) col[j] = clampc(t.s - 1 + j, 0, rw - 1) - qx0;
+        for (int r = 0; r < NY; ++r) {
+          const float* row = I + r * rxc;
+          float h = __fmul_rn(row[col[0]], t.c[0]);
+          h = __fadd_rn(h, __fmul_rn(row[col[1]], t.c[1]));
+          h = __fadd_rn(h, __fmul_rn(row[col[2]], t.c[2]));
+          h = __fadd_rn(h, __fmul_rn(row[col[3]], t.c[3]));
+          H2[r * kFusedTX + tid] = h;
+        }
+        const bool simd2 = x * cn + ce < dw * cn / 4 * 4;
+#pragma unroll
+        for (int yy = 0; yy < kFusedTY; ++yy) {
+          const CubicTap ty = t2y[k * kFusedTY + yy];
+          int rr[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rr[j] = clampc(ty.s - 1 + j, 0, rh - 1) - qy0;
+          const float h0 = H2[rr[0] * kFusedTX + tid], h1 = H2[rr[1] * kFusedTX + tid];
+          const float h2 = H2[rr[2] * kFusedTX + tid], h3 = H2[rr[3] * kFusedTX + tid];
+          float v;
+          if (simd2) {
+            const float t3 = __fmul_rn(h3, ty.c[3]);
+            const float t2 = __fadd_rn(__fmul_rn(h2, ty.c[2]), t3);
+            const float t1 = __fadd_rn(__fmul_rn(h1, ty.c[1]), t2);
+            v = __fadd_rn(__fmul_rn(h0, ty.c[0]), t1);
+          } else {
+            v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty.c[0]), __fmul_rn(h1, ty.c[1])), __fmul_rn(h2, ty.c[2])),
+                          __fmul_rn(h3, ty.c[3]));
+          }
+          sum[yy] = k == 0 ? v : __fadd_rn(sum[yy], v);
+        }
+      }
+    }
+    if (x < dw) {
+      float* o = dst + ((int64_t)f * nch + c) * plane + (int64_t)y0 * dw + x;
+#pragma unroll
+      for (int yy = 0; yy < kFusedTY; ++yy)
+        if (y0 + yy < dh) o[(int64_t)yy * dw] = __fdiv_rn(sum[yy], (float)ns);
+    }
+  }
+}
+
+// LDS bytes of resize_cubic_fused_mean<TY> for these scales (and their extents into a), 0 when
+// over its budget.  Extents: T consecutive outputs read source taps floor((x + 0.5) s - 0.5) - 1 ..
+// + 2, at most floor((T - 1) s) + 1 + 4 distinct indices (+1 for the f32 rounding of the coordinate).
+static size_t fused_lds(CubicFusedArgs& a, int ty) {
+  int rx = 0, ry = 0, lr = 0;
+  for (int k = 0; k < a.ns; ++k) {
+    const int nx = (int)std::floor((kFusedTX - 1) * a.s2x[k]) + 7;
+    const int ny = (int)std::floor((ty - 1) * a.s2y[k]) + 7;
+    rx = std::max(rx, std::min(nx, a.rw[k]));
+    ry = std::max(ry, std::min(ny, a.rh[k]));
+    lr = std::max(lr, std::min((int)std::floor((ny - 1) * a.s1y[k]) + 7, a.lh[k]));
+  }
+  a.rx_cap = rx;
+  a.ry_cap = ry;
+  a.lr_cap = lr;
+  const size_t lds = (size_t)a.ns * (rx + ry + ty) * sizeof(CubicTap) +
+                     4 * ((size_t)lr * rx + (size_t)ry * rx + (size_t)ry * kFusedTX);
+  return lds <= 96 * 1024 ? lds : 0;
+}
+
+size_t cubic_fused_lds(CubicFusedArgs& a) {
+  const size_t l = fused_lds(a, 16);
+  return l ? l : fused_lds(a, 8);
+}
+
+int launch_resize_cubic_fused_mean(CubicFusedArgs a, float* dst, int32_t n, int32_t dh, int32_t dw, int32_t npaf,
+                                   int32_t nheat, hipStream_t st, bool* taken) {
+  *taken = false;
+  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
+    set_error("resize_cubic_fused_mean: 1..OP_MAX_SCALES scales");
+    return OP_ERR_INVALID;
+  }
+  int ty = 16;
+  size_t lds = fused_lds(a, 16);
+  if (!lds) {
+    ty = 8;
+    lds = fused_lds(a, 8);
+  }
+  if (!lds) return OP_OK;
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)resize_cubic_fused_mean<16>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)resize_cubic_fused_mean<8>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    attr = true;
+  }
+  const int ngroups = (npaf + nheat + kFusedG - 1) / kFusedG;
+  const dim3 grid((unsigned)((dw + kFusedTX - 1) / kFusedTX), (unsigned)((dh + ty - 1) / ty), (unsigned)(n * ngroups));
+  if (ty == 16)
+    hipLaunchKernelGGL(resize_cubic_fused_mean<16>, grid, dim3(256), lds, st, a, dst, dh, dw, npaf, nheat);
+  else
+    hipLaunchKernelGGL(resize_cubic_fused_mean<8>, grid, dim3(256), lds, st, a, dst, dh, dw, npaf, nheat);
+  OP_AFTER_LAUNCH("resize_cubic_fused_mean", st);
+  OP_HIP_CHECK(hipGetLastError());
+  *taken = true;
+  return OP_OK;
+}
+
 // Generic cv2.resize(INTER_CUBIC) of a cn-channel uint8 image (row stride sstride bytes) to a
 // contiguous dh x dw x cn image (the stage-level ABI op_resize_cubic).
 __global__ __launch_bounds__(256) void resize_cubic_u8(const uint8_t* __restrict__ src, int64_t sstride, int sh, int sw,

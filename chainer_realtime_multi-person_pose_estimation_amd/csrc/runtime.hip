@@ -2646,7 +2646,28 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
     mid_off[k + 1] = mid_off[k] + (size_t)n * phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT);
   }
   const int64_t fplanes = (int64_t)(OP_N_PAF + OP_N_HEAT) * h * w;  // floats per frame of psum
-  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, mid_off[ns] * 4, "precise_mid"));
+  // round 4: both map resizes and the scale mean in one pass from each scale's last-stage maps
+  // (copied planar into d_pmid at low_off[k]) when the fused kernel's tiles fit LDS
+  // (OP_CUBIC_FUSED=0: the two-pass path, an A/B and parity aid); bit-identical either way
+  CubicFusedArgs fa{};
+  size_t low_off[OP_MAX_SCALES + 1] = {0};
+  fa.ns = ns;
+  for (int k = 0; k < ns; ++k) {
+    fa.lh[k] = phs[k] / ds;
+    fa.lw[k] = pws[k] / ds;
+    fa.pw[k] = pws[k];
+    fa.rh[k] = rhs[k];
+    fa.rw[k] = rws[k];
+    fa.s1x[k] = 1.0 / ((double)pws[k] / (double)fa.lw[k]);  // cv_cubic_scale (cvcubic.hpp)
+    fa.s1y[k] = 1.0 / ((double)phs[k] / (double)fa.lh[k]);
+    fa.s2x[k] = 1.0 / ((double)w / (double)rws[k]);
+    fa.s2y[k] = 1.0 / ((double)h / (double)rhs[k]);
+    fa.lframe[k] = (int64_t)(OP_N_PAF + OP_N_HEAT) * fa.lh[k] * fa.lw[k];
+    low_off[k + 1] = low_off[k] + (size_t)n * fa.lframe[k];
+  }
+  const char* fenv = getenv("OP_CUBIC_FUSED");
+  const bool fused = !(fenv && atoi(fenv) == 0) && cubic_fused_lds(fa) > 0;
+  RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, (fused ? low_off[ns] : mid_off[ns]) * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;
   for (int k = 0; k < ns; ++k) {
@@ -2682,7 +2703,16 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       paf_off = kCatPaf;
       heat_off = kCatHeat;
     }
-    {
+    if (fused) {
+      float* low = c->d_pmid + low_off[k];
+      fa.low[k] = low;
+      RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+        RC(launch_maps_planar(mbase + paf_off, mrow, mpx, mframe, lh, lw, OP_N_PAF, low, 0, OP_N_PAF + OP_N_HEAT, n,
+                              c->stream));
+        return launch_maps_planar(mbase + heat_off, mrow, mpx, mframe, lh, lw, OP_N_HEAT, low, OP_N_PAF,
+                                  OP_N_PAF + OP_N_HEAT, n, c->stream);
+      }));
+    } else {
       // :461 / :465 cubic to the padded size (the heat by fx = fy = downscale: the same mapping),
       // stored planar (cn, ph, pw) so the second resize reads coalesced rows; kept for every scale
       // and frame until the fused second pass below; every frame of the scale in one launch per map
@@ -2700,7 +2730,18 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   }
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
   // order and divided by the scale count: one pass per frame over the PAF and heat planes
-  for (int f = 0; f < n; ++f) {
+  census_add(fused ? OP_CENSUS_CUBIC_FUSED : OP_CENSUS_CUBIC_TWO_PASS);
+  if (fused) {
+    bool taken = false;
+    RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+      return launch_resize_cubic_fused_mean(fa, c->d_psum, n, h, w, OP_N_PAF, OP_N_HEAT, c->stream, &taken);
+    }));
+    if (!taken) {
+      set_error("detect_precise: fused map resize refused a checked shape");
+      return OP_ERR_STATE;
+    }
+  }
+  for (int f = 0; f < n && !fused; ++f) {
     CubicMeanArgs a{};
     a.ns = ns;
     for (int k = 0; k < ns; ++k) {

@@ -128,3 +128,45 @@ def test_loaded_full_resolution_postprocess(lib, rand_weights):
         c.use_staged_maps(False)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("shape,n", [((H, W), 3), ((481, 643), 2), ((96, 128), 2)])
+def test_fused_map_resize_equals_two_pass(lib, rand_weights, shape, n, monkeypatch):
+    """Round 4: detect_precise's two cubic map resizes per scale and the scale mean run as one fused
+    pass (precise.hip resize_cubic_fused_mean: the padded-size maps never reach HBM).  It restates
+    the two-pass kernels' f32 operations in their order, so the averaged maps of a staged batch are
+    BIT-IDENTICAL with OP_CUBIC_FUSED=0 (the two-pass path, held to the oracle above).  96x128 frames
+    upsample their scale-2 crop ~7.7x in the second resize: the fused tile then exceeds LDS and the
+    two-pass path runs (census)."""
+    Wt = _weights(rand_weights)
+    limits = lib.OpLimits()
+    limits.max_peaks_per_joint = 2048
+    c = lib.Context(0, None, limits)
+    h, w = shape
+    try:
+        c.set_weights(Wt)
+        c.set_batch_invariant(True)
+        frames = np.stack([_crowd_frame(11 + i)[:h, :w] for i in range(n)])
+        out = {}
+        for fused in ("1", "0"):
+            monkeypatch.setenv("OP_CUBIC_FUSED", fused)
+            c.stage_frames(frames)
+            lib.conv_census(reset=True)
+            try:
+                c.run_staged_precise()
+            except IndexError:
+                pass
+            c.synchronize()
+            cen = lib.conv_census(reset=True)
+            out[fused] = (c.fetch_maps(0, n), cen)
+        (p1, h1), cen1 = out["1"]
+        (p0, h0), cen0 = out["0"]
+        assert cen0["cubic_two_pass"] == 1 and cen0["cubic_fused"] == 0
+        if shape == (96, 128):
+            assert cen1["cubic_two_pass"] == 1 and cen1["cubic_fused"] == 0
+        else:
+            assert cen1["cubic_fused"] == 1 and cen1["cubic_two_pass"] == 0
+        assert p1.shape == (n, 38, h, w) and h1.shape == (n, 19, h, w)
+        assert np.array_equal(p1, p0) and np.array_equal(h1, h0)
+    finally:
+        c.close()
