@@ -224,7 +224,7 @@ struct CubicFusedArgs {
   int rh[OP_MAX_SCALES], rw[OP_MAX_SCALES];              // crop = second resize's source size
   double s1x[OP_MAX_SCALES], s1y[OP_MAX_SCALES];         // first resize: cv_cubic_scale(pw, lw), (ph, lh)
   double s2x[OP_MAX_SCALES], s2y[OP_MAX_SCALES];         // second: cv_cubic_scale(w, rw), (h, rh)
-  int rx_cap, ry_cap, lr_cap;                            // LDS extents (host bounds)
+  int rx_cap, ry_cap, lr_cap, pc_cap;                    // LDS extents (host bounds)
 };
 // false (and nothing launched) when a scale's tile extents exceed the kernel's LDS budget: the
 // caller then runs the two-pass path

@@ -24,6 +24,7 @@
 #include <array>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <cstdlib>
 #include <vector>
 
@@ -507,6 +508,56 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
   if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
 }
 
+// Split-K partials of a conv with the fused 2x2 max-pool (round 4: pooled 3x3 launches that fill
+// few CUs, one frame's conv2_2 / conv3_4): one thread per (pooled pixel, 4 channels) sums the
+// partials of its 4 conv pixels in split order onto the bias, then ReLU, the split round trip and
+// the max as the pooled epilogue of conv_m16k_bf16x3<true>, and stores the pooled split value.
+__global__ __launch_bounds__(256) void conv_m16_splitk_reduce_pool(SplitConvShape s, SplitConvGroup g,
+                                                                   BigTiling tl) {
+  const int q = g.cop / 4;
+  const int ho = s.h / 2, wo = s.w / 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)s.n * ho * wo * q) return;
+  const int64_t Po = i / q;
+  const int co = (int)(i - Po * q) * 4;
+  if (co >= g.cout_store) return;
+  const int f = (int)(Po / ((int64_t)ho * wo)), pp = (int)(Po - (int64_t)f * ho * wo);
+  const int yo = pp / wo, xo = pp - yo * wo;
+  const floatx4 bv = *(const floatx4*)(g.bias + co);
+  floatx4 m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t P = ((int64_t)f * s.h + 2 * yo + (k >> 1)) * s.w + 2 * xo + (k & 1);
+    floatx4 v = bv;
+    for (int sp = 0; sp < tl.ksplit; ++sp) {
+      const floatx4 a = *(const floatx4*)(tl.ws + ((int64_t)sp * tl.total + P) * g.cop + co);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += a[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float fv = v[e];
+      if (s.relu) fv = fv > 0.0f ? fv : 0.0f;
+      const __bf16 h16 = (__bf16)fv;
+      const float rc = (float)h16 + (float)(__bf16)(fv - (float)h16);
+      m[e] = k == 0 ? rc : fmaxf(m[e], rc);
+    }
+  }
+  const int wp_out = wo + 2 * s.pout, hp_out = ho + 2 * s.pout;
+  char* d = (char*)g.out + (((int64_t)f * hp_out + yo + s.pout) * wp_out + (xo + s.pout)) * (int64_t)s.cs_out * 4 +
+            (co >> 3) * 32 + (co & 7) * 2;
+  u16x4g vh, vl;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h16 = (__bf16)m[e];
+    const __bf16 l16v = (__bf16)(m[e] - (float)h16);
+    vh[e] = __builtin_bit_cast(unsigned short, h16);
+    vl[e] = __builtin_bit_cast(unsigned short, l16v);
+  }
+  *(u16x4g*)d = vh;
+  *(u16x4g*)(d + 16) = vl;
+}
+
 // ---- 3x3: conv_m16k_bf16x3 (conv_m16k.hpp) ----
 
 // ---- host side ----
@@ -709,7 +760,7 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   t.ksplit = 1;
   t.ws = nullptr;
   static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
-  if (!pool && s.splitk) {
+  if (s.splitk && (!pool || s.groups == 1)) {
     const int pairs = s.c16 / 2;
     int S = 1;
     if (ks_force > 0) S = pairs % ks_force == 0 ? ks_force : 1;
@@ -742,7 +793,11 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   } else
     hipLaunchKernelGGL(conv_m16k_bf16x3<false>, grid, dim3(256), lds, st, s, g[0], g1, t);
   OP_AFTER_LAUNCH("conv_m16k_bf16x3", st);
-  if (t.ksplit > 1) {
+  if (t.ksplit > 1 && pool) {
+    const int64_t items = (int64_t)s.n * (s.h / 2) * (s.w / 2) * (g[0].cop / 4);
+    hipLaunchKernelGGL(conv_m16_splitk_reduce_pool, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, g[0], t);
+    OP_AFTER_LAUNCH("conv_m16_splitk_reduce_pool", st);
+  } else if (t.ksplit > 1) {
     int cop_max = g[0].cop;
     if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
     const int64_t items = (int64_t)t.total * (cop_max / 4);
@@ -827,17 +882,31 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       auto rounds = [](const BigTiling& t) -> int {
         return t.xpu ? ((t.per_unit + t.xpu - 1) / t.xpu + 31) / 32 : (t.units * t.per_unit + 255) / 256;
       };
+      // Split-K (launches that leave CUs idle: one frame, one crop; never in batch-invariant mode):
+      // the input chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce).  Round
+      // 4: the tile size and the split S are chosen together -- a workgroup's time is ~ its chunks x
+      // (2 + NPX), a launch's ~ rounds x that, plus ~0.2 of a unit per split for the partials and the
+      // reduce launch (OP_M16_SPLIT_GAMMA) -- over S dividing the chunk count (2 .. 16, not just
+      // 8 / 4 / 2): one 368x368 frame's Mconv2-5 take NPX 3 x S 8 (176 workgroups, one chunk each)
+      // instead of NPX 2 x S 4 (136 workgroups, two chunks each), Mconv1 NPX 4 x S 12.
+      static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
+      static const bool joint = !(getenv("OP_M16_JOINT") && atoi(getenv("OP_M16_JOINT")) == 0);  // A/B aid
+      static const double gamma = getenv("OP_M16_SPLIT_GAMMA") ? atof(getenv("OP_M16_SPLIT_GAMMA")) : 0.2;
+      auto wgs_of = [](const BigTiling& t) -> int {
+        return t.xpu ? 8 * ((t.per_unit + t.xpu - 1) / t.xpu) : t.units * t.per_unit;
+      };
       // every launch shape is evaluated once (the tilings loop over tiles) and cached
       static std::mutex sel_mu;
-      static std::map<std::array<int, 5>, std::pair<int, BigTiling>> sel_cache;
-      const std::array<int, 5> key{s.n, s.h, s.w, s.groups, cop_max};
-      int npx = 10;
+      static std::map<std::array<int, 7>, std::tuple<int, BigTiling, int>> sel_cache;
+      const std::array<int, 7> key{s.n, s.h, s.w, s.groups, cop_max, s.c16, s.splitk};
+      int npx = 10, S = 1;
       {
         std::lock_guard<std::mutex> lk(sel_mu);
         auto it = sel_cache.find(key);
         if (it != sel_cache.end()) {
-          npx = it->second.first;
-          tl = it->second.second;
+          npx = std::get<0>(it->second);
+          tl = std::get<1>(it->second);
+          S = std::get<2>(it->second);
         } else {
           if (force != 10) {
             int best = rounds(tl) * (2 + 10);
@@ -855,7 +924,36 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
               }
             }
           }
-          sel_cache[key] = {npx, tl};
+          if (s.splitk && ks_force > 0) {
+            S = s.c16 % ks_force == 0 ? ks_force : 1;
+          } else if (s.splitk && !joint) {  // round 3's rule: the no-split tile, the largest S of 8 / 4 / 2 that fits
+            for (int cand : {8, 4, 2})
+              if (s.c16 % cand == 0 && wgs_of(tl) * cand <= 256) {
+                S = cand;
+                break;
+              }
+          } else if (s.splitk && wgs_of(tl) < 256) {
+            double best = (double)rounds(tl) * s.c16 * (2 + npx);
+            for (int cand : {10, 8, 6, 5, 4, 3, 2}) {
+              if (force && cand != force) continue;
+              BigConfig k{7, 1, 8, 128, 1, 1};
+              k.cap_px = 64 * cand;
+              BigTiling tc{};
+              if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
+              for (int sp : {2, 3, 4, 6, 8, 12, 16}) {
+                if (s.c16 % sp) continue;
+                const int r = (wgs_of(tc) * sp + 255) / 256;
+                const double cost = (double)r * (s.c16 / sp) * (2 + cand) + gamma * sp;
+                if (cost < best) {
+                  best = cost;
+                  npx = cand;
+                  tl = tc;
+                  S = sp;
+                }
+              }
+            }
+          }
+          sel_cache[key] = std::make_tuple(npx, tl, S);
         }
       }
       if (plain_order) tl.xpu = 0;
@@ -865,28 +963,13 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         return OP_ERR_STATE;
       }
       *taken = 1;
-      // Split-K for launches that still leave most CUs idle (one frame, one crop): the input
-      // chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce), since a
-      // workgroup's time is mostly its per-chunk, per-tap-pair work, not its pixel count
-      static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
-      const int wgs = tl.xpu ? 8 * ((tl.per_unit + tl.xpu - 1) / tl.xpu) : tl.units * tl.per_unit;
       tl.ksplit = 1;
       tl.ws = nullptr;
-      if (s.splitk) {
-        int S = 1;
-        if (ks_force > 0) S = s.c16 % ks_force == 0 ? ks_force : 1;
-        else
-          for (int cand : {8, 4, 2})
-            if (s.c16 % cand == 0 && wgs * cand <= 256) {
-              S = cand;
-              break;
-            }
-        if (S > 1) {
-          float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
-          if (ws) {
-            tl.ksplit = S;
-            tl.ws = ws;
-          }
+      if (s.splitk && S > 1) {
+        float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
+        if (ws) {
+          tl.ksplit = S;
+          tl.ws = ws;
         }
       }
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];

@@ -68,8 +68,9 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
   // weights: 16 1-KiB pieces per step; wave w copies j = 4w .. 4w+3: chunk j/8, plane (j/2)%4, half j%2
   const int64_t wplane = (int64_t)g.cop * 16;
   const int64_t wstep = 4 * wplane;  // one (chunk, tap)
-  // split-K (tl.ksplit > 1, not with the pooled epilogue): chunk pairs [cp0, cp1) of this workgroup
-  const int nsplit = (!POOL && tl.ksplit > 1) ? tl.ksplit : 1;
+  // split-K (tl.ksplit > 1): chunk pairs [cp0, cp1) of this workgroup (pooled launches too, round 4:
+  // conv_m16_splitk_reduce_pool then sums, pools and stores)
+  const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
   const int split = nsplit > 1 ? (int)blockIdx.y : 0;
   const int cp0 = split * (s.c16 / 2 / nsplit), cp1 = cp0 + s.c16 / 2 / nsplit;
   const int n_it = cp1 * KSQ;
@@ -171,6 +172,23 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
   }
   wait_vmcnt<0>();
 
+  if (nsplit > 1) {  // raw partials in raster order (conv_m16_splitk_reduce finishes them)
+    const int wsc = max(g0.cop, g1.cop);
+    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
+#pragma unroll
+    for (int pb = 0; pb < NPX; ++pb) {
+      const int b = pg * NPX + pb;
+      const int r = b / TCB, c = (b % TCB) * 16 + l16;
+      if (r >= rows_here || c >= cols_here) continue;
+      const int64_t P = ((int64_t)frame * s.h + y0 + r) * s.w + x0 + c;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
+        if (co < g.cop) *(floatx4*)(wsg + P * wsc + co) = acc[cb][pb];
+      }
+    }
+    return;
+  }
   if constexpr (POOL) {
     // rows (b, b+2) = tile rows (r, r+1); columns (l16, l16 ^ 1) = lanes (l, l ^ 1)
     const int wp_out = s.w / 2 + 2 * s.pout;
@@ -217,23 +235,6 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
     return;
   }
 
-  if (nsplit > 1) {  // raw partials in raster order (conv_m16_splitk_reduce finishes them)
-    const int wsc = max(g0.cop, g1.cop);
-    float* const wsg = tl.ws + ((int64_t)split * s.groups + grp) * (int64_t)tl.total * wsc;
-#pragma unroll
-    for (int pb = 0; pb < NPX; ++pb) {
-      const int b = pg * NPX + pb;
-      const int r = b / TCB, c = (b % TCB) * 16 + l16;
-      if (r >= rows_here || c >= cols_here) continue;
-      const int64_t P = ((int64_t)frame * s.h + y0 + r) * s.w + x0 + c;
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-        if (co < g.cop) *(floatx4*)(wsg + P * wsc + co) = acc[cb][pb];
-      }
-    }
-    return;
-  }
   const int wp_out = s.w + 2 * s.pout;
   const int hp_out = s.h + 2 * s.pout;
 #pragma unroll

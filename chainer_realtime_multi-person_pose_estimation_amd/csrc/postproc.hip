@@ -555,10 +555,26 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
     const int ja = s.limbs[l][0], jb = s.limbs[l][1];
     const int64_t fl = (int64_t)f * OP_N_LIMBS + l;
     const int K = b.conn_cnt[fl];
-    for (int c = 0; c < K && status == OP_OK; ++c) {
-      const int ia = b.conn_ab[2 * (fl * b.maxp + c)];
-      const int ib = b.conn_ab[2 * (fl * b.maxp + c) + 1];
-      const double score = b.conn_score[fl * b.maxp + c];
+    // round 4: the limb's connections (ids, score, both peaks' scores) are fetched 64 at a time, one
+    // per lane, and broadcast from registers: the loop over connections no longer waits on a chain
+    // of dependent global loads per connection (one frame with 7 people: 74 -> ? us)
+    for (int cb = 0; cb < K && status == OP_OK; cb += 64) {
+    int my_ia = 0, my_ib = 0;
+    double my_sc = 0.0, my_pa = 0.0, my_pb = 0.0;
+    if (cb + lane < K) {
+      const int64_t q = fl * b.maxp + cb + lane;
+      my_ia = b.conn_ab[2 * q];
+      my_ib = b.conn_ab[2 * q + 1];
+      my_sc = b.conn_score[q];
+      my_pa = pscore(ja, my_ia);
+      my_pb = pscore(jb, my_ib);
+    }
+    const int ce = min(K - cb, 64);
+    for (int c = 0; c < ce && status == OP_OK; ++c) {
+      const int ia = __shfl(my_ia, c);
+      const int ib = __shfl(my_ib, c);
+      const double score = __shfl(my_sc, c);
+      const double psa = __shfl(my_pa, c), psb = __shfl(my_pb, c);  // pscore(ja, ia), pscore(jb, ib)
       int found = 0, f0 = -1, f1 = -1;
       for (int s0 = 0; s0 < S; s0 += 64) {
         const int r = s0 + lane;
@@ -581,7 +597,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
         if (lane == 0 && ids[f0][jb] != ib) {
           ids[f0][jb] = (IdT)ib;
           sc[f0][1] = __dadd_rn(sc[f0][1], 1.0);
-          sc[f0][0] = __dadd_rn(sc[f0][0], __dadd_rn(pscore(jb, ib), score));
+          sc[f0][0] = __dadd_rn(sc[f0][0], __dadd_rn(psb, score));
         }
       } else if (found == 2) {
         const bool both = lane < OP_N_JOINTS && ids[f0][lane] >= 0 && ids[f1][lane] >= 0;
@@ -621,11 +637,11 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
             if (ids[t][ja] == -1) {
               ids[t][ja] = (IdT)ia;
               sc[t][1] = __dadd_rn(sc[t][1], 1.0);
-              sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(pscore(ja, ia), score));
+              sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(psa, score));
             } else if (ids[t][jb] == -1) {
               ids[t][jb] = (IdT)ib;
               sc[t][1] = __dadd_rn(sc[t][1], 1.0);
-              sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(pscore(jb, ib), score));
+              sc[t][0] = __dadd_rn(sc[t][0], __dadd_rn(psb, score));
             }
           }
         }
@@ -637,11 +653,12 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
         if (lane < OP_N_JOINTS) ids[S][lane] = (IdT)(lane == ja ? ia : (lane == jb ? ib : -1));
         if (lane == 0) {
           sc[S][1] = 2.0;
-          sc[S][0] = __dadd_rn(__dadd_rn(pscore(ja, ia), pscore(jb, ib)), score);
+          sc[S][0] = __dadd_rn(__dadd_rn(psa, psb), score);
         }
         ++S;
       }
       __syncthreads();
+    }
     }
   }
   // keep filter (pose_detector.py:248) + subsets_to_pose_array + subsets dump, ordered compaction

@@ -354,6 +354,9 @@ int launch_maps_planar(const float* src, int64_t sstride, int32_t pstride, int64
 // 1280x720 frame ~1.04 GB of padded-size map writes and reads become 210 MB of output writes.
 // kFusedTY = TY output rows per block: 16, or 8 where the scales' crops are large against the
 // output (second-resize ratios over ~1.1) and 16 rows' extents would not fit the LDS budget.
+// Loop order: scales outer, the block's kFusedG channels inner, the running sums of all of them
+// in registers (sum[g][y]); per scale the taps are made once and the G channels' low-res patches
+// are loaded into LDS in one round of global loads.
 constexpr int kFusedTX = 256, kFusedG = 8;
 template <int kFusedTY>
 __global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a, float* __restrict__ dst, int dh,
@@ -362,107 +365,127 @@ __global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a,
   const int nch = npaf + nheat;
   const int ngroups = (nch + kFusedG - 1) / kFusedG;
   const int f = blockIdx.z / ngroups, c0 = (blockIdx.z - f * ngroups) * kFusedG;
+  const int ng = min(kFusedG, nch - c0);
   const int x0 = blockIdx.x * kFusedTX, y0 = blockIdx.y * kFusedTY;
   const int tid = threadIdx.x, x = x0 + tid;
   const int xl = min(x0 + kFusedTX - 1, dw - 1), yl = min(y0 + kFusedTY - 1, dh - 1);
-  const int ns = a.ns, rxc = a.rx_cap, ryc = a.ry_cap;
-  CubicTap* t1x = (CubicTap*)lds;                  // [ns][rx_cap]
-  CubicTap* t1y = t1x + ns * rxc;                  // [ns][ry_cap]
-  CubicTap* t2y = t1y + ns * ryc;                  // [ns][TY]
-  float* H1 = (float*)(t2y + ns * kFusedTY);       // [lr_cap][rx_cap]
-  float* I = H1 + a.lr_cap * rxc;                  // [ry_cap][rx_cap]
-  float* H2 = I + ryc * rxc;                       // [ry_cap][TX]
-  // per scale: the crop columns / rows the tile reads and the low-res rows those rows read (in LDS:
-  // the scale loop below is not unrolled, so per-scale register arrays would go to scratch)
-  __shared__ int rq[6][OP_MAX_SCALES];  // qx0, nqx, qy0, nqy, l0, nl
-  for (int k = 0; k < ns; ++k) {
-    const int rw = a.rw[k], rh = a.rh[k];
+  const int rxc = a.rx_cap, ryc = a.ry_cap, lrc = a.lr_cap, pcc = a.pc_cap;
+  CubicTap* t1x = (CubicTap*)lds;          // [rx_cap]   first resize, crop columns
+  CubicTap* t1y = t1x + rxc;               // [ry_cap]   first resize, crop rows
+  CubicTap* t2y = t1y + ryc;               // [TY]       second resize, output rows
+  float* P = (float*)(t2y + kFusedTY);     // [G][lr_cap][pc_cap] low-res patches
+  float* H1 = P + kFusedG * lrc * pcc;     // [lr_cap][rx_cap]
+  float* I = H1 + lrc * rxc;               // [ry_cap][rx_cap]
+  float* H2 = I + ryc * rxc;               // [ry_cap][TX]
+  float sum[kFusedG][kFusedTY];
+  for (int k = 0; k < a.ns; ++k) {
+    const int lw = a.lw[k], lh = a.lh[k], rw = a.rw[k], rh = a.rh[k];
+    // the crop columns / rows the tile reads, the low-res rows and columns those read (uniform)
     const int qx0 = clampc(cv_cubic_tap_s(x0, a.s2x[k]).s - 1, 0, rw - 1);
+    const int NX = clampc(cv_cubic_tap_s(xl, a.s2x[k]).s + 2, 0, rw - 1) - qx0 + 1;
     const int qy0 = clampc(cv_cubic_tap_s(y0, a.s2y[k]).s - 1, 0, rh - 1);
-    const int nqy = clampc(cv_cubic_tap_s(yl, a.s2y[k]).s + 2, 0, rh - 1) - qy0 + 1;
-    const int nqx = clampc(cv_cubic_tap_s(xl, a.s2x[k]).s + 2, 0, rw - 1) - qx0 + 1;
-    const int l0 = clampc(cv_cubic_tap_s(qy0, a.s1y[k]).s - 1, 0, a.lh[k] - 1);
-    if (tid == 0) {
-      rq[0][k] = qx0;
-      rq[1][k] = nqx;
-      rq[2][k] = qy0;
-      rq[3][k] = nqy;
-      rq[4][k] = l0;
-      rq[5][k] = clampc(cv_cubic_tap_s(qy0 + nqy - 1, a.s1y[k]).s + 2, 0, a.lh[k] - 1) - l0 + 1;
+    const int NY = clampc(cv_cubic_tap_s(yl, a.s2y[k]).s + 2, 0, rh - 1) - qy0 + 1;
+    const int l0 = clampc(cv_cubic_tap_s(qy0, a.s1y[k]).s - 1, 0, lh - 1);
+    const int NL = clampc(cv_cubic_tap_s(qy0 + NY - 1, a.s1y[k]).s + 2, 0, lh - 1) - l0 + 1;
+    const int p0 = clampc(cv_cubic_tap_s(qx0, a.s1x[k]).s - 1, 0, lw - 1);
+    const int NP = clampc(cv_cubic_tap_s(qx0 + NX - 1, a.s1x[k]).s + 2, 0, lw - 1) - p0 + 1;
+    const bool fits = NX <= rxc && NY <= ryc && NL <= lrc && NP <= pcc;  // never false (host bounds)
+    __syncthreads();  // the previous scale's last step c has read I; its taps are no longer read
+    if (fits) {
+      for (int i = tid; i < NX; i += 256) t1x[i] = cv_cubic_tap_s(qx0 + i, a.s1x[k]);
+      for (int i = tid; i < NY; i += 256) t1y[i] = cv_cubic_tap_s(qy0 + i, a.s1y[k]);
+      if (tid < kFusedTY) t2y[tid] = cv_cubic_tap_s(min(y0 + tid, dh - 1), a.s2y[k]);
+      const float* src = a.low[k] + (int64_t)f * a.lframe[k] + (int64_t)c0 * lh * lw + (int64_t)l0 * lw + p0;
+      for (int j = tid; j < ng * NL * pcc; j += 256) {
+        const int row = j / pcc, col = j - row * pcc;  // row = g * NL + l
+        const int g = row / NL, l = row - g * NL;
+        if (col < NP) P[(g * lrc + l) * pcc + col] = src[((int64_t)g * lh + l) * lw + col];
+      }
     }
-    for (int i = tid; i < nqx; i += 256) t1x[k * rxc + i] = cv_cubic_tap_s(qx0 + i, a.s1x[k]);
-    for (int i = tid; i < nqy; i += 256) t1y[k * ryc + i] = cv_cubic_tap_s(qy0 + i, a.s1y[k]);
-    if (tid < kFusedTY) t2y[k * kFusedTY + tid] = cv_cubic_tap_s(min(y0 + tid, dh - 1), a.s2y[k]);
-  }
-  __syncthreads();
-  const int64_t plane = (int64_t)dh * dw;
-  for (int g = 0; g < kFusedG; ++g) {
-    const int c = c0 + g;
-    if (c >= nch) break;
-    const bool paf = c < npaf;
-    const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
-    float sum[kFusedTY];
-    for (int k = 0; k < ns; ++k) {
-      const int lw = a.lw[k], lh = a.lh[k], rw = a.rw[k], rh = a.rh[k];
-      const int qx0 = rq[0][k], NX = rq[1][k], qy0 = rq[2][k], NY = rq[3][k], l0 = rq[4][k], NL = rq[5][k];
-      if (NX > rxc || NY > ryc || NL > a.lr_cap) {  // never (host bounds); loud if they were wrong
-        if (x < dw)
-          for (int yy = 0; yy < kFusedTY; ++yy) sum[yy] = __builtin_nanf("");
-        continue;
-      }
-      const float* src = a.low[k] + (int64_t)f * a.lframe[k] + (int64_t)c * lh * lw;
-      // a. H1[l][i]: low-res row l0 + l, crop column qx0 + i (resize_cubic_f32_up's horizontal sum)
-      for (int j = tid; j < NL * NX; j += 256) {
-        const int l = j / NX, i = j - l * NX;
-        const CubicTap t = t1x[k * rxc + i];
-        const float* row = src + (int64_t)(l0 + l) * lw;
-        float h = __fmul_rn(row[clampc(t.s - 1, 0, lw - 1)], t.c[0]);
-        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s, 0, lw - 1)], t.c[1]));
-        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s + 1, 0, lw - 1)], t.c[2]));
-        h = __fadd_rn(h, __fmul_rn(row[clampc(t.s + 2, 0, lw - 1)], t.c[3]));
-        H1[l * rxc + i] = h;
-      }
-      __syncthreads();  // also: every thread's step c of the previous scale / channel has read I
-      // b. I[r][i]: the first resize's output at (qy0 + r, qx0 + i), its vertical order over pw x cn
-      const int simd1 = a.pw[k] * cn / 4 * 4;
-      for (int j = tid; j < NY * NX; j += 256) {
-        const int r = j / NX, i = j - r * NX;
-        const CubicTap t = t1y[k * ryc + r];
-        const float h0 = H1[(clampc(t.s - 1, 0, lh - 1) - l0) * rxc + i];
-        const float h1 = H1[(clampc(t.s, 0, lh - 1) - l0) * rxc + i];
-        const float h2 = H1[(clampc(t.s + 1, 0, lh - 1) - l0) * rxc + i];
-        const float h3 = H1[(clampc(t.s + 2, 0, lh - 1) - l0) * rxc + i];
-        float v;
-        if ((qx0 + i) * cn + ce < simd1) {
-          const float t3 = __fmul_rn(h3, t.c[3]);
-          const float t2 = __fadd_rn(__fmul_rn(h2, t.c[2]), t3);
-          const float t1 = __fadd_rn(__fmul_rn(h1, t.c[1]), t2);
-          v = __fadd_rn(__fmul_rn(h0, t.c[0]), t1);
-        } else {
-          v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, t.c[0]), __fmul_rn(h1, t.c[1])), __fmul_rn(h2, t.c[2])),
-                        __fmul_rn(h3, t.c[3]));
+    const CubicTap tx2 = cv_cubic_tap_s(min(x, dw - 1), a.s2x[k]);
+    int col2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col2[j] = clampc(tx2.s - 1 + j, 0, rw - 1) - qx0;
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < kFusedG; ++g) {  // unrolled: sum[g] stays in registers
+      if (g >= ng) break;
+      const int c = c0 + g;
+      const bool paf = c < npaf;
+      const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+      if (fits) {
+        // a. H1[l][i]: low-res row l0 + l, crop column qx0 + i (resize_cubic_f32_up's horizontal sum);
+        //    work items of 4 rows x 1 column (16 independent LDS reads each)
+        const float* pg = P + g * lrc * pcc;
+        const int NLB = (NL + 3) >> 2;
+        for (int j = tid; j < NX * NLB; j += 256) {
+          const int lb = j / NX, i = j - lb * NX;
+          const CubicTap t = t1x[i];
+          int cc[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cc[e] = clampc(t.s - 1 + e, 0, lw - 1) - p0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int l = min(4 * lb + q, NL - 1);  // past the last row: recompute it (same value)
+            const float* row = pg + l * pcc;
+            float h = __fmul_rn(row[cc[0]], t.c[0]);
+            h = __fadd_rn(h, __fmul_rn(row[cc[1]], t.c[1]));
+            h = __fadd_rn(h, __fmul_rn(row[cc[2]], t.c[2]));
+            h = __fadd_rn(h, __fmul_rn(row[cc[3]], t.c[3]));
+            H1[l * rxc + i] = h;
+          }
         }
-        I[r * rxc + i] = v;
+        __syncthreads();
+        // b. I[r][i]: the first resize's output at (qy0 + r, qx0 + i), its vertical order over pw x cn;
+        //    work items of 4 rows x 1 column
+        const int simd1 = a.pw[k] * cn / 4 * 4;
+        const int NYB = (NY + 3) >> 2;
+        for (int j = tid; j < NX * NYB; j += 256) {
+          const int rb = j / NX, i = j - rb * NX;
+          const bool simd = (qx0 + i) * cn + ce < simd1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int r = min(4 * rb + q, NY - 1);
+            const CubicTap t = t1y[r];
+            const float h0 = H1[(clampc(t.s - 1, 0, lh - 1) - l0) * rxc + i];
+            const float h1 = H1[(clampc(t.s, 0, lh - 1) - l0) * rxc + i];
+            const float h2 = H1[(clampc(t.s + 1, 0, lh - 1) - l0) * rxc + i];
+            const float h3 = H1[(clampc(t.s + 2, 0, lh - 1) - l0) * rxc + i];
+            float v;
+            if (simd) {
+              const float t3 = __fmul_rn(h3, t.c[3]);
+              const float t2 = __fadd_rn(__fmul_rn(h2, t.c[2]), t3);
+              const float t1 = __fadd_rn(__fmul_rn(h1, t.c[1]), t2);
+              v = __fadd_rn(__fmul_rn(h0, t.c[0]), t1);
+            } else {
+              v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, t.c[0]), __fmul_rn(h1, t.c[1])), __fmul_rn(h2, t.c[2])),
+                            __fmul_rn(h3, t.c[3]));
+            }
+            I[r * rxc + i] = v;
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
       // c + d: this thread's output column (no barrier: H2's column is the thread's own)
       if (x < dw) {
-        const CubicTap t = cv_cubic_tap_s(x, a.s2x[k]);
-        int col[4];
+        if (!fits) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) col[j] = clampc(t.s - 1 + j, 0, rw - 1) - qx0;
+          for (int yy = 0; yy < kFusedTY; ++yy) sum[g][yy] = __builtin_nanf("");
+          continue;
+        }
+#pragma unroll 4
         for (int r = 0; r < NY; ++r) {
           const float* row = I + r * rxc;
-          float h = __fmul_rn(row[col[0]], t.c[0]);
-          h = __fadd_rn(h, __fmul_rn(row[col[1]], t.c[1]));
-          h = __fadd_rn(h, __fmul_rn(row[col[2]], t.c[2]));
-          h = __fadd_rn(h, __fmul_rn(row[col[3]], t.c[3]));
+          float h = __fmul_rn(row[col2[0]], tx2.c[0]);
+          h = __fadd_rn(h, __fmul_rn(row[col2[1]], tx2.c[1]));
+          h = __fadd_rn(h, __fmul_rn(row[col2[2]], tx2.c[2]));
+          h = __fadd_rn(h, __fmul_rn(row[col2[3]], tx2.c[3]));
           H2[r * kFusedTX + tid] = h;
         }
         const bool simd2 = x * cn + ce < dw * cn / 4 * 4;
 #pragma unroll
         for (int yy = 0; yy < kFusedTY; ++yy) {
-          const CubicTap ty = t2y[k * kFusedTY + yy];
+          const CubicTap ty = t2y[yy];
           int rr[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) rr[j] = clampc(ty.s - 1 + j, 0, rh - 1) - qy0;
@@ -478,15 +501,20 @@ __global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a,
             v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty.c[0]), __fmul_rn(h1, ty.c[1])), __fmul_rn(h2, ty.c[2])),
                           __fmul_rn(h3, ty.c[3]));
           }
-          sum[yy] = k == 0 ? v : __fadd_rn(sum[yy], v);
+          sum[g][yy] = k == 0 ? v : __fadd_rn(sum[g][yy], v);
         }
       }
     }
-    if (x < dw) {
-      float* o = dst + ((int64_t)f * nch + c) * plane + (int64_t)y0 * dw + x;
+  }
+  if (x < dw) {
+    const int64_t plane = (int64_t)dh * dw;
+#pragma unroll
+    for (int g = 0; g < kFusedG; ++g) {
+      if (g >= ng) break;
+      float* o = dst + ((int64_t)f * nch + c0 + g) * plane + (int64_t)y0 * dw + x;
 #pragma unroll
       for (int yy = 0; yy < kFusedTY; ++yy)
-        if (y0 + yy < dh) o[(int64_t)yy * dw] = __fdiv_rn(sum[yy], (float)ns);
+        if (y0 + yy < dh) o[(int64_t)yy * dw] = __fdiv_rn(sum[g][yy], (float)a.ns);
     }
   }
 }
@@ -495,19 +523,21 @@ __global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a,
 // over its budget.  Extents: T consecutive outputs read source taps floor((x + 0.5) s - 0.5) - 1 ..
 // + 2, at most floor((T - 1) s) + 1 + 4 distinct indices (+1 for the f32 rounding of the coordinate).
 static size_t fused_lds(CubicFusedArgs& a, int ty) {
-  int rx = 0, ry = 0, lr = 0;
+  int rx = 0, ry = 0, lr = 0, pc = 0;
   for (int k = 0; k < a.ns; ++k) {
-    const int nx = (int)std::floor((kFusedTX - 1) * a.s2x[k]) + 7;
-    const int ny = (int)std::floor((ty - 1) * a.s2y[k]) + 7;
-    rx = std::max(rx, std::min(nx, a.rw[k]));
-    ry = std::max(ry, std::min(ny, a.rh[k]));
+    const int nx = std::min((int)std::floor((kFusedTX - 1) * a.s2x[k]) + 7, a.rw[k]);
+    const int ny = std::min((int)std::floor((ty - 1) * a.s2y[k]) + 7, a.rh[k]);
+    rx = std::max(rx, nx);
+    ry = std::max(ry, ny);
     lr = std::max(lr, std::min((int)std::floor((ny - 1) * a.s1y[k]) + 7, a.lh[k]));
+    pc = std::max(pc, std::min((int)std::floor((nx - 1) * a.s1x[k]) + 7, a.lw[k]));
   }
   a.rx_cap = rx;
   a.ry_cap = ry;
   a.lr_cap = lr;
-  const size_t lds = (size_t)a.ns * (rx + ry + ty) * sizeof(CubicTap) +
-                     4 * ((size_t)lr * rx + (size_t)ry * rx + (size_t)ry * kFusedTX);
+  a.pc_cap = pc;
+  const size_t lds = (size_t)(rx + ry + ty) * sizeof(CubicTap) +
+                     4 * ((size_t)kFusedG * lr * pc + (size_t)lr * rx + (size_t)ry * rx + (size_t)ry * kFusedTX);
   return lds <= 96 * 1024 ? lds : 0;
 }
 
