@@ -715,7 +715,12 @@ static bool m16k_tiling(const SplitConvShape& s, int groups, int cop_max, bool p
   // 8 x 32 tiles, or 4 x 48 where they waste fewer MFMA lanes (narrow maps; not with the pool)
   const double u32 = (double)s.w / (((s.w + 31) / 32) * 32) * s.h / (((s.h + 7) / 8) * 8);
   const double u48 = (double)s.w / (((s.w + 47) / 48) * 48) * s.h / (((s.h + 3) / 4) * 4);
-  const bool w48 = !pool && !no48 && u48 > u32 + 0.02;
+  // round 4: on narrow maps where both tile shapes use the lanes equally (the 82 x 46 maps of
+  // 1280x720 frames: 85 % either way), 4 x 48 tiles rather than falling back to conv_big below --
+  // large launches then run conv_m16r (same arithmetic order as conv_m16k: a frame's bits do not
+  // depend on the batch); OP_M16K_TIE48=0 restores the fallback (A/B aid)
+  static const bool tie48 = !(getenv("OP_M16K_TIE48") && atoi(getenv("OP_M16K_TIE48")) == 0);
+  const bool w48 = !pool && !no48 && (u48 > u32 + 0.02 || (tie48 && s.w < 128 && u48 >= u32 - 1e-9));
   t.tc = w48 ? 48 : 32;
   t.tr = w48 ? 4 : 8;
   t.tiles_x = (s.w + t.tc - 1) / t.tc;

@@ -194,9 +194,18 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
       }
     }
     if (next) {
-      // this wave's pieces of the next pair were issued by tap 4; younger than them are only the
-      // weight loads of taps 5..8 (2 CBW each): waiting down to 8 outstanding covers every piece
-      wait_vmcnt<8>();
+      // this wave's pieces of the next pair were issued by tap HSTEPS - 1; younger than them are
+      // only the weight loads of taps HSTEPS..8 (2 CBW each, load_a): waiting down to that many
+      // outstanding covers every piece and keeps those weight loads in flight across the barrier
+      // (round 3 waited down to 8, which also drained half of them -- advisor finding;
+      // M16R_WAIT8 builds that for the A/B)
+#ifdef M16R_WAIT8
+      constexpr int kYounger = 8;
+#else
+      constexpr int kYounger = (9 - HSTEPS) * 2 * CBW;
+#endif
+      static_assert(kYounger >= 0 && kYounger <= 63, "vmcnt literal");
+      wait_vmcnt<kYounger>();
       __builtin_amdgcn_s_barrier();  // every wave's pieces landed; this pair's buffer is free
       asm volatile("" ::: "memory");
     }

@@ -357,7 +357,7 @@ int launch_maps_planar(const float* src, int64_t sstride, int32_t pstride, int64
 // Loop order: scales outer, the block's kFusedG channels inner, the running sums of all of them
 // in registers (sum[g][y]); per scale the taps are made once and the G channels' low-res patches
 // are loaded into LDS in one round of global loads.
-constexpr int kFusedTX = 256, kFusedG = 8;
+constexpr int kFusedTX = 256, kFusedG = 2;  // G unrolled: 8 made a ~117 KB kernel (I-cache bound, 12 ms)
 template <int kFusedTY>
 __global__ __launch_bounds__(256) void resize_cubic_fused_mean(CubicFusedArgs a, float* __restrict__ dst, int dh,
                                                                int dw, int npaf, int nheat) {
