@@ -962,6 +962,14 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         }
       }
       if (plain_order) tl.xpu = 0;
+      // channel tiles that share their input (one group, Mconv1's 256 channels): a pixel tile's
+      // tiles back to back on one XCD (OP_M16_PAIR=0: one channel tile per XCD set, round 3)
+      static const bool m16_pair = !(getenv("OP_M16_PAIR") && atoi(getenv("OP_M16_PAIR")) == 0);
+      tl.pair = 1;
+      if (m16_pair && tl.xpu && s.groups == 1 && tl.co_tiles > 1 && 8 % tl.co_tiles == 0) {
+        tl.pair = tl.co_tiles;
+        tl.xpu = 8;
+      }
       tl.zeros = device_zeros();
       if (!tl.zeros) {
         set_error("conv_m16_bf16x3: conv_big_device_init was not called for this device");

@@ -36,9 +36,14 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int lin = blockIdx.x;
   int unit, widx;
   if (tl.xpu) {
+    // XCD set su runs weight sets su*P .. su*P+P-1 (P = tl.pair, default 1); with P > 1 (Mconv1: its
+    // two channel tiles read the same 192-channel input) one pixel tile's P channel tiles are
+    // consecutive slots of one XCD, so its halo is fetched once into that XCD's L2
     const int xcd = lin & 7, slot = lin >> 3;
-    unit = xcd / tl.xpu;
-    widx = slot * tl.xpu + (xcd - unit * tl.xpu);
+    const int P = tl.pair > 1 ? tl.pair : 1;
+    const int su = xcd / tl.xpu, q = slot / P, xo = xcd - su * tl.xpu;
+    unit = su * P + (slot - q * P);
+    widx = q * tl.xpu + xo;
   } else {
     unit = lin / tl.per_unit;
     widx = lin - unit * tl.per_unit;
@@ -280,7 +285,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
   const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
                        : 4 * 4 * 128 * 16 + 4 * 32 * 1024;   // ring + 4 halo planes (32-KiB stride)
-  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu)
+  const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu * std::max(tl.pair, 1))
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
   switch (npx) {

@@ -8,4 +8,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4p
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/b1prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --batch 1 --steps 40 --warmup 5 --no-cpu-baseline --no-variants --no-profile > $O/b1prof.log 2>&1 || exit $?
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u bench.py --precise --frame 720x1280 > $O/c4.log 2>&1 || exit $?
+timeout -k 10 900 python3 -u tools/ab_lib.py 3 OP_M16_PAIR=1 OP_M16_PAIR=0 > $O/ab_pair.log 2>&1 || exit $?
 echo done
