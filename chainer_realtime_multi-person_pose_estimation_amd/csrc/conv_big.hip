@@ -884,8 +884,23 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       // workgroups in one round instead of 106 at 2.4x the work each; 40-57 frames: 8, two
       // rounds of 512-px tiles instead of two of 640).
       static const int force = getenv("OP_M16_NPX") ? atoi(getenv("OP_M16_NPX")) : 0;  // A/B aid
+      // channel tiles that share their input (one group, Mconv1's 256 channels): a pixel tile's
+      // tiles back to back on one XCD -- OFF by default (OP_M16_PAIR=1 selects it): neutral in a
+      // 3-run A/B on the headline (1869.3 vs 1868.0 frames/s, profiles/r04/ab_r04i_mconv1_pair.log),
+      // so the round-3 mapping (one channel tile per XCD set) stays.  Applied to every candidate
+      // tiling before it is costed (the grid grows to whole XCD rounds)
+      static const bool m16_pair = getenv("OP_M16_PAIR") && atoi(getenv("OP_M16_PAIR")) == 1;
+      auto pairmaj = [&](BigTiling& t) {
+        t.pair = 1;
+        if (m16_pair && !plain_order && t.xpu && s.groups == 1 && t.co_tiles > 1 && 8 % t.co_tiles == 0) {
+          t.pair = t.co_tiles;
+          t.xpu = 8;
+        }
+      };
+      pairmaj(tl);
       auto rounds = [](const BigTiling& t) -> int {
-        return t.xpu ? ((t.per_unit + t.xpu - 1) / t.xpu + 31) / 32 : (t.units * t.per_unit + 255) / 256;
+        const int P = t.pair > 1 ? t.pair : 1;
+        return t.xpu ? ((t.per_unit + t.xpu - 1) / t.xpu * P + 31) / 32 : (t.units * t.per_unit + 255) / 256;
       };
       // Split-K (launches that leave CUs idle: one frame, one crop; never in batch-invariant mode):
       // the input chunks are divided over blockIdx.y (f32 partials + conv_m16_splitk_reduce).  Round
@@ -898,7 +913,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       static const bool joint = !(getenv("OP_M16_JOINT") && atoi(getenv("OP_M16_JOINT")) == 0);  // A/B aid
       static const double gamma = getenv("OP_M16_SPLIT_GAMMA") ? atof(getenv("OP_M16_SPLIT_GAMMA")) : 0.2;
       auto wgs_of = [](const BigTiling& t) -> int {
-        return t.xpu ? 8 * ((t.per_unit + t.xpu - 1) / t.xpu) : t.units * t.per_unit;
+        return t.xpu ? 8 * ((t.per_unit + t.xpu - 1) / t.xpu) * (t.pair > 1 ? t.pair : 1) : t.units * t.per_unit;
       };
       // every launch shape is evaluated once (the tilings loop over tiles) and cached
       static std::mutex sel_mu;
@@ -921,6 +936,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
               k.cap_px = 64 * cand;
               BigTiling tc{};
               if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
+              pairmaj(tc);
               const int cost = rounds(tc) * (2 + cand);
               if (force || cost < best) {
                 best = cost;
@@ -945,6 +961,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
               k.cap_px = 64 * cand;
               BigTiling tc{};
               if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
+              pairmaj(tc);
               for (int sp : {2, 3, 4, 6, 8, 12, 16}) {
                 if (s.c16 % sp) continue;
                 const int r = (wgs_of(tc) * sp + 255) / 256;
@@ -961,14 +978,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
           sel_cache[key] = std::make_tuple(npx, tl, S);
         }
       }
-      if (plain_order) tl.xpu = 0;
-      // channel tiles that share their input (one group, Mconv1's 256 channels): a pixel tile's
-      // tiles back to back on one XCD (OP_M16_PAIR=0: one channel tile per XCD set, round 3)
-      static const bool m16_pair = !(getenv("OP_M16_PAIR") && atoi(getenv("OP_M16_PAIR")) == 0);
-      tl.pair = 1;
-      if (m16_pair && tl.xpu && s.groups == 1 && tl.co_tiles > 1 && 8 % tl.co_tiles == 0) {
-        tl.pair = tl.co_tiles;
-        tl.xpu = 8;
+      if (plain_order) {
+        tl.xpu = 0;
+        tl.pair = 1;
       }
       tl.zeros = device_zeros();
       if (!tl.zeros) {

@@ -746,10 +746,16 @@ __device__ __forceinline__ bool may_reach(float v, float thresh) {
 
 // R > 0: radius fixed at compile time (register-blocked passes, NV outputs per thread); R == 0: any
 // radius <= kMaxR given at run time (one output per thread).
+// Block order (round 4): a 1-D grid where XCD x (= linear block id mod 8) runs every tile of every
+// joint of frames x, x + 8, ...: the 18 joints' blocks of a frame read the same low-res pixel
+// records (38 + 19 of 64 interleaved channels per 256-B record), so those lines come from HBM
+// once, into that XCD's L2, instead of once per XCD.  n_frames: frames of the launch; tx, ty:
+// tiles per plane.
 template <class Src, int R>
 __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const double* __restrict__ w, int rr,
                                                   float thresh, int cap, int32_t* __restrict__ stage_key,
-                                                  float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt) {
+                                                  float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt,
+                                                  int n_frames, int tx, int ty) {
   constexpr int kTP = kFU + 2;  // vertical-pass output pitch (16-byte aligned rows)
   constexpr int kHP = kFT + 4;  // filtered-map pitch
   constexpr int NB = 4;         // outputs per thread in the register-blocked passes
@@ -758,9 +764,14 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
   __shared__ AxisTap rt[kFU], ct[kFU];
   __shared__ int wlo[2], whi[2];
   const int r = R > 0 ? R : rr;
-  const int fj = blockIdx.z;
-  const int f = fj / OP_N_JOINTS, j = fj - f * OP_N_JOINTS;
-  const int x0 = blockIdx.x * kFT, y0 = blockIdx.y * kFT;
+  const int per_frame = tx * ty * OP_N_JOINTS;
+  const int lin = blockIdx.x, xcd = lin & 7, slot = lin >> 3;
+  const int f = (slot / per_frame) * 8 + xcd;
+  if (f >= n_frames) return;
+  const int within = slot - (slot / per_frame) * per_frame;
+  const int j = within / (tx * ty), t = within - j * (tx * ty);
+  const int fj = f * OP_N_JOINTS + j;
+  const int x0 = (t % tx) * kFT, y0 = (t / tx) * kFT;
   const int hr = min(kFT + 2, mh + 1 - y0);  // filtered rows needed: image rows y0-1 .. <= mh-1
   const int hc = min(kFT + 2, mw + 1 - x0);
   const int ur = hr + 2 * r, uc = hc + 2 * r;
@@ -993,13 +1004,14 @@ template <class Src>
 static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
   const int planes = s.n * OP_N_JOINTS;
   OP_HIP_CHECK(hipMemsetAsync(b.peak_cnt, 0, sizeof(int32_t) * planes, st));
-  dim3 g((unsigned)((s.mw + kFT - 1) / kFT), (unsigned)((s.mh + kFT - 1) / kFT), (unsigned)planes);
+  const int tx = (s.mw + kFT - 1) / kFT, ty = (s.mh + kFT - 1) / kFT;
+  const dim3 g((unsigned)(8 * ((s.n + 7) / 8) * tx * ty * OP_N_JOINTS));
   if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
     hipLaunchKernelGGL((heat_fused<Src, 10>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
-                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty);
   else
     hipLaunchKernelGGL((heat_fused<Src, 0>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
-                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt);
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty);
   OP_AFTER_LAUNCH("heat_fused<Src>", st);
   if (b.maxp <= 2048) {
     hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,

@@ -2646,9 +2646,11 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
     mid_off[k + 1] = mid_off[k] + (size_t)n * phs[k] * pws[k] * (OP_N_PAF + OP_N_HEAT);
   }
   const int64_t fplanes = (int64_t)(OP_N_PAF + OP_N_HEAT) * h * w;  // floats per frame of psum
-  // round 4: both map resizes and the scale mean in one pass from each scale's last-stage maps
-  // (copied planar into d_pmid at low_off[k]) when the fused kernel's tiles fit LDS
-  // (OP_CUBIC_FUSED=0: the two-pass path, an A/B and parity aid); bit-identical either way
+  // round 4 experiment, OFF by default: both map resizes and the scale mean in one pass from each
+  // scale's last-stage maps (copied planar into d_pmid at low_off[k]) -- bit-identical, but it
+  // recomputes each tile's crop halo and makes ~4.5x the VALU instructions of the two-pass path,
+  // which is VALU/issue-bound rather than HBM-bound: 12.5 vs 11.3 ms per 16 1280x720 frames
+  // (SQ_INSTS_VALU, profiles/r04/c4_fused_cubic_not_kept.md).  OP_CUBIC_FUSED=1 selects it.
   CubicFusedArgs fa{};
   size_t low_off[OP_MAX_SCALES + 1] = {0};
   fa.ns = ns;
@@ -2666,7 +2668,7 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
     low_off[k + 1] = low_off[k] + (size_t)n * fa.lframe[k];
   }
   const char* fenv = getenv("OP_CUBIC_FUSED");
-  const bool fused = !(fenv && atoi(fenv) == 0) && cubic_fused_lds(fa) > 0;
+  const bool fused = fenv && atoi(fenv) == 1 && cubic_fused_lds(fa) > 0;
   RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, (fused ? low_off[ns] : mid_off[ns]) * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;

@@ -132,12 +132,13 @@ def test_loaded_full_resolution_postprocess(lib, rand_weights):
 
 @pytest.mark.parametrize("shape,n", [((H, W), 3), ((481, 643), 2), ((96, 128), 2)])
 def test_fused_map_resize_equals_two_pass(lib, rand_weights, shape, n, monkeypatch):
-    """Round 4: detect_precise's two cubic map resizes per scale and the scale mean run as one fused
-    pass (precise.hip resize_cubic_fused_mean: the padded-size maps never reach HBM).  It restates
-    the two-pass kernels' f32 operations in their order, so the averaged maps of a staged batch are
-    BIT-IDENTICAL with OP_CUBIC_FUSED=0 (the two-pass path, held to the oracle above).  96x128 frames
-    upsample their scale-2 crop ~7.7x in the second resize: the fused tile then exceeds LDS and the
-    two-pass path runs (census)."""
+    """Round 4 experiment (opt-in, OP_CUBIC_FUSED=1; the default is the two-pass path, which measured
+    faster): detect_precise's two cubic map resizes per scale and the scale mean as one fused pass
+    (precise.hip resize_cubic_fused_mean: the padded-size maps never reach HBM).  It restates the
+    two-pass kernels' f32 operations in their order, so the averaged maps of a staged batch are
+    BIT-IDENTICAL with the two-pass path (held to the oracle above).  96x128 frames upsample their
+    scale-2 crop ~7.7x in the second resize: the fused tile then exceeds LDS and the two-pass path
+    runs (census)."""
     Wt = _weights(rand_weights)
     limits = lib.OpLimits()
     limits.max_peaks_per_joint = 2048

@@ -1,7 +1,10 @@
 #!/bin/bash
-# Round 4: fused cubic (G 2) parity + C4 trace; batch-1 trace.
+# Round 4: L2-stream micro (Winograd costing); fused cubic (G 2) parity + C4 trace; batch-1 trace;
+# C4 line; Mconv1 pair-major A/B.
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/r04i; mkdir -p $O
+timeout -k 10 120 tools/micro/l2_mfma_stream > $O/l2_mfma_stream_4MiB.log 2>&1 || exit $?
+timeout -k 10 120 tools/micro/l2_mfma_stream 16777216 > $O/l2_mfma_stream_16MiB.log 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest -q --timeout 600 --timeout-method thread tests/test_gpu_precise_full.py > $O/tests.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --precise --frame 720x1280 --steps 3 --warmup 1 --no-variants --no-profile > $O/c4prof.log 2>&1 || exit $?
