@@ -93,6 +93,22 @@ struct ConvShape {
 
 int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st);
 
+// a branch's two closing 1x1 convs fused, exact f32 (conv.hip conv_head_f32)
+struct HeadF32Shape {
+  int32_t n, h, w, pin, cs_in, pout, cs_out;
+  int32_t c8;      // input channels / 8
+  int32_t co1;     // layer a's channels (a multiple of 128)
+  int32_t groups;  // 1 or 2 (the two branches)
+};
+struct HeadF32Group {
+  const float* in;  // padded NHWC input, offset by the group's first input channel
+  const float *w1, *b1, *w2, *b2;  // packed [c8][cop][8] weights and biases of layers a and b
+  int32_t cop1, cop2;
+  float* out;  // padded NHWC output, offset by the group's first output channel
+  int32_t cout_store;
+};
+int launch_conv_head_f32(const HeadF32Shape& s, const HeadF32Group* g, hipStream_t st);
+
 // ---- 3xBF16 split path (conv_bf16x3.hip) ----
 struct SplitConvGroup {
   const float* in;      // split NHWC input, offset by the group's first input channel (multiple of 16)

@@ -161,6 +161,148 @@ int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st) {
   }
 }
 
+// A branch's two closing 1x1 convs in one launch, exact f32 (conv5_4 + conv5_5, CocoPoseNet.py:
+// 162-165; Mconv6 + Mconv7, :181-184 and the later stages): in -> a (bias, ReLU) -> b (bias) -> out,
+// the intermediate kept in registers.  A wave owns 32 pixels; layer a runs in groups of 128 channels
+// (4 blocks of 32, K = the input channels), and each group's ReLU'd accumulators feed layer b's
+// K loop directly as B operands: the D layout of v_mfma_f32_32x32x2_f32 gives lane (pixel, hi)
+// channels (r&3) + 8(r>>2) + 4hi of a block in register r, i.e. for chunk c8 = 4 block + (r>>2)
+// and MFMA j = r&3 the k-pair {8c8 + j, 8c8 + 4 + j} that conv_mfma_f32 contracts with the same
+// packed weights [c8][co][8].  Both layers therefore accumulate in conv_mfma_f32's order and the
+// output is bit-identical to the two-launch path, without the intermediate's HBM round trip
+// (stage 1: 512 channels per pixel).
+template <int CB2>
+__global__ __launch_bounds__(256) void conv_head_f32(HeadF32Shape s, HeadF32Group g0, HeadF32Group g1) {
+  const HeadF32Group g = blockIdx.z == 0 ? g0 : g1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hw = s.h * s.w;
+  const int total = s.n * hw;
+  const int px_base = (blockIdx.x * 4 + wave) * 32;
+  if (px_base >= total) return;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int wp_in = s.w + 2 * s.pin, hp_in = s.h + 2 * s.pin;
+  const float* bptr;
+  {
+    int p = px_base + l32;
+    if (p >= total) p = total - 1;
+    const int n = p / hw, rem = p - n * hw;
+    const int y = rem / s.w, x = rem - y * s.w;
+    bptr = g.in + ((int64_t)(n * hp_in + y + s.pin) * wp_in + (x + s.pin)) * s.cs_in + 4 * hi;
+  }
+  const int64_t wstep1 = (int64_t)g.cop1 * 8, wstep2 = (int64_t)g.cop2 * 8;
+
+  floatx16 accb[CB2];
+#pragma unroll
+  for (int cb = 0; cb < CB2; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accb[cb][r] = 0.0f;
+
+  for (int grp = 0; grp < s.co1 / 128; ++grp) {
+    floatx16 acca[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acca[cb][r] = 0.0f;
+    const float* aptr = g.w1 + (int64_t)(grp * 128 + l32) * 8 + 4 * hi;
+    auto load = [&](floatx4(&a)[4], floatx4& b, int c) {
+      if (c >= s.c8) c = s.c8 - 1;  // tail prefetch: a valid address, never consumed
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) a[cb] = *(const floatx4*)(aptr + c * wstep1 + cb * 256);
+      b = *(const floatx4*)(bptr + c * 8);
+    };
+    auto mma = [&](const floatx4(&a)[4], const floatx4& b) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acca[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][j], b[j], acca[cb], 0, 0, 0);
+    };
+    floatx4 a0[4], a1[4], b0, b1;
+    load(a0, b0, 0);
+    load(a1, b1, 1);
+    int c = 0;
+    for (; c + 2 <= s.c8; c += 2) {
+      mma(a0, b0);
+      load(a0, b0, c + 2);
+      mma(a1, b1);
+      load(a1, b1, c + 3);
+    }
+    if (c < s.c8) mma(a0, b0);
+    // layer a's bias + ReLU, in place
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 bv = *(const floatx4*)(g.b1 + grp * 128 + cb * 32 + 8 * q + 4 * hi);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = acca[cb][4 * q + e] + bv[e];
+          acca[cb][4 * q + e] = v > 0.0f ? v : 0.0f;
+        }
+      }
+    // layer b over this group's 128 channels: chunk c8 = 16 grp + 4 cb + q
+    const float* a2ptr = g.w2 + (int64_t)l32 * 8 + 4 * hi;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c8 = 16 * grp + 4 * cb + q;
+        floatx4 a2[CB2];
+#pragma unroll
+        for (int cb2 = 0; cb2 < CB2; ++cb2) a2[cb2] = *(const floatx4*)(a2ptr + c8 * wstep2 + cb2 * 256);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int cb2 = 0; cb2 < CB2; ++cb2)
+            accb[cb2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[cb2][j], acca[cb][4 * q + j], accb[cb2], 0, 0, 0);
+      }
+  }
+
+  // epilogue (conv_mfma_f32's): layer b's bias, no ReLU
+  const int p = px_base + l32;
+  if (p >= total) return;
+  const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
+  const int n = p / hw, rem = p - n * hw;
+  const int y = rem / s.w, x = rem - y * s.w;
+  float* optr = g.out + ((int64_t)(n * hp_out + y + s.pout) * wp_out + (x + s.pout)) * s.cs_out;
+#pragma unroll
+  for (int cb = 0; cb < CB2; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int co = cb * 32 + 8 * q + 4 * hi;
+      if (co >= g.cout_store) continue;
+      const floatx4 bv = *(const floatx4*)(g.b2 + co);
+      floatx4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = accb[cb][4 * q + e] + bv[e];
+      *(floatx4*)(optr + co) = v;
+    }
+}
+
+int launch_conv_head_f32(const HeadF32Shape& s, const HeadF32Group* g, hipStream_t st) {
+  // the kernel's assumptions (no bounds checks inside)
+  if (s.c8 <= 0 || s.co1 <= 0 || s.co1 % 128 || s.cs_in % 4 || s.cs_out % 4 || s.groups < 1 || s.groups > 2) {
+    set_error("launch_conv_head_f32: unsupported shape");
+    return OP_ERR_INVALID;
+  }
+  const int cop2 = g[0].cop2;
+  for (int i = 0; i < s.groups; ++i) {
+    if (g[i].cop1 < s.co1 || g[i].cop1 % 64 || g[i].cop2 != cop2 || (cop2 != 32 && cop2 != 64) ||
+        g[i].cout_store % 4 || g[i].cout_store > cop2) {
+      set_error("launch_conv_head_f32: channel padding");
+      return OP_ERR_INVALID;
+    }
+  }
+  const int64_t total = (int64_t)s.n * s.h * s.w;
+  const dim3 grid((unsigned)((total + 127) / 128), 1, (unsigned)s.groups);
+  const HeadF32Group& g1 = s.groups > 1 ? g[1] : g[0];
+  if (cop2 == 64) hipLaunchKernelGGL((conv_head_f32<2>), grid, dim3(256), 0, st, s, g[0], g1);
+  else hipLaunchKernelGGL((conv_head_f32<1>), grid, dim3(256), 0, st, s, g[0], g1);
+  OP_AFTER_LAUNCH("conv_head_f32", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 // F.max_pooling_2d(h, ksize=2, stride=2) (CocoPoseNet.py:138,141,146); sizes are even here
 // (multiples of 8, pose_detector.py:57-73), so cover_all adds no extra window.
 __global__ __launch_bounds__(256) void maxpool2_nhwc(const float* __restrict__ in, int pin, float* __restrict__ out,

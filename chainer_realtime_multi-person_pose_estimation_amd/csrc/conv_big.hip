@@ -421,7 +421,9 @@ struct SplitkWs {
   size_t floats = 0;
   size_t short_by = 0;  // largest request refused during capture
   std::vector<float*> retired;  // outgrown buffers: a graph captured earlier may still read them
+  int32_t* cnt = nullptr;       // kSplitkCounters zeroed arrival counters (BigTiling::cnt)
 };
+constexpr int kSplitkCounters = 1 << 16;
 static std::mutex g_ws_mu;
 static std::map<hipStream_t, SplitkWs> g_ws;
 
@@ -434,12 +436,31 @@ static float* splitk_ws(hipStream_t st, size_t floats) {
     e.short_by = std::max(e.short_by, floats);
     return nullptr;
   }
+  if (!e.cnt) {  // allocated with the first workspace, outside capture; kept for the stream's life
+    int32_t* c = nullptr;
+    if (hipMalloc(&c, kSplitkCounters * sizeof(int32_t)) != hipSuccess) return nullptr;
+    if (hipMemset(c, 0, kSplitkCounters * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(c);
+      return nullptr;
+    }
+    e.cnt = c;
+  }
   float* p = nullptr;
   if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
   if (e.p) e.retired.push_back(e.p);
   e.p = p;
   e.floats = floats;
   return p;
+}
+
+// The stream's arrival counters when a launch of `tiles` (weight set, pixel tile) pairs can finish
+// its split-K in the conv kernel (OP_SPLITK_INKERNEL=0: always the reduce launch, an A/B aid).
+static int32_t* splitk_counters(hipStream_t st, int64_t tiles) {
+  const char* e = getenv("OP_SPLITK_INKERNEL");  // read per launch: the parity test A/Bs it in-process
+  if ((e && atoi(e) == 0) || tiles > kSplitkCounters) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws.find(st);
+  return it == g_ws.end() ? nullptr : it->second.cnt;
 }
 
 size_t splitk_ws_capture_short(hipStream_t st) {
@@ -465,6 +486,7 @@ void splitk_ws_release(hipStream_t st) {
   auto it = g_ws.find(st);
   if (it == g_ws.end()) return;
   if (it->second.p) (void)hipFree(it->second.p);
+  if (it->second.cnt) (void)hipFree(it->second.cnt);
   for (float* p : it->second.retired) (void)hipFree(p);
   g_ws.erase(it);
 }
@@ -480,32 +502,7 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
   if (i >= (int64_t)tl.total * q) return;
   const int P = (int)(i / q), co = (int)(i - (int64_t)P * q) * 4;
   if (co >= g.cout_store) return;
-  const int wsc = max(g0.cop, g1.cop);
-  floatx4 v = *(const floatx4*)(g.bias + co);
-  for (int sp = 0; sp < tl.ksplit; ++sp) {
-    const floatx4 a = *(const floatx4*)(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] += a[e];
-  }
-  const int f = P / tl.hw, pp = P - f * tl.hw;
-  const int y = pp / s.w, x = pp - y * s.w;
-  const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
-  const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
-  char* d = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
-            ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * split_pixel_stride(s.out_planar, s.cs_out) +
-            (co >> 3) * 2 * out_pc + (co & 7) * 2;
-  u16x4g vh, vl;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (s.relu) v[e] = v[e] > 0.0f ? v[e] : 0.0f;
-    const __bf16 h16 = (__bf16)v[e];
-    const __bf16 l16v = (__bf16)(v[e] - (float)h16);
-    vh[e] = __builtin_bit_cast(unsigned short, h16);
-    vl[e] = __builtin_bit_cast(unsigned short, l16v);
-  }
-  *(u16x4g*)d = vh;
-  *(u16x4g*)(d + out_pc) = vl;
-  if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
+  splitk_reduce_item(s, g, grp, tl, max(g0.cop, g1.cop), P, co);
 }
 
 // Split-K partials of a conv with the fused 2x2 max-pool (round 4: pooled 3x3 launches that fill
@@ -764,6 +761,7 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   BigTiling t = tl;
   t.ksplit = 1;
   t.ws = nullptr;
+  t.cnt = nullptr;
   static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
   if (s.splitk && (!pool || s.groups == 1)) {
     const int pairs = s.c16 / 2;
@@ -784,12 +782,14 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
       if (ws) {
         t.ksplit = S;
         t.ws = ws;
+        if (!pool) t.cnt = splitk_counters(st, (int64_t)t.units * t.per_unit);
       }
     }
   }
   const dim3 grid(blocks, (unsigned)t.ksplit);
   census_add(pool ? OP_CENSUS_3X3_POOL : tl.tc == 48 ? OP_CENSUS_3X3_W48 : OP_CENSUS_3X3_W32);
   if (t.ksplit > 1) census_add(OP_CENSUS_3X3_SPLITK);
+  if (t.cnt) census_add(OP_CENSUS_SPLITK_INKERNEL);
   if (pool)
     hipLaunchKernelGGL(conv_m16k_bf16x3<true>, grid, dim3(256), lds, st, s, g[0], g1, t);
   else if (tl.tc == 48) {
@@ -802,7 +802,7 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
     const int64_t items = (int64_t)s.n * (s.h / 2) * (s.w / 2) * (g[0].cop / 4);
     hipLaunchKernelGGL(conv_m16_splitk_reduce_pool, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, g[0], t);
     OP_AFTER_LAUNCH("conv_m16_splitk_reduce_pool", st);
-  } else if (t.ksplit > 1) {
+  } else if (t.ksplit > 1 && !t.cnt) {
     int cop_max = g[0].cop;
     if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
     const int64_t items = (int64_t)t.total * (cop_max / 4);
@@ -990,22 +990,25 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       *taken = 1;
       tl.ksplit = 1;
       tl.ws = nullptr;
+      tl.cnt = nullptr;
       if (s.splitk && S > 1) {
         float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
         if (ws) {
           tl.ksplit = S;
           tl.ws = ws;
+          tl.cnt = splitk_counters(st, (int64_t)tl.units * tl.per_unit);
         }
       }
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
       census_add(npx);
       if (tl.ksplit > 1) census_add(OP_CENSUS_7X7_SPLITK);
+      if (tl.cnt) census_add(OP_CENSUS_SPLITK_INKERNEL);
       if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
       if (tl.fa_tiles) census_add(OP_CENSUS_7X7_FRAME_ALIGNED);
       if (tl.pitch == s.w + 6) census_add(OP_CENSUS_7X7_TIGHT);
       const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
       if (rc != OP_OK) return rc;
-      if (tl.ksplit > 1) {
+      if (tl.ksplit > 1 && !tl.cnt) {
         OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
         const int64_t items = (int64_t)tl.total * (cop_max / 4);
         hipLaunchKernelGGL(conv_m16_splitk_reduce, dim3((unsigned)((items + 255) / 256), (unsigned)s.groups), dim3(256),

@@ -29,6 +29,8 @@ struct BigTiling {
                              // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
   int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
   float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
+  int32_t* cnt;              // non-null: split-K finished in the conv kernel (splitk_arrive), one
+                             // arrival counter per (weight set, pixel tile), zero between launches
   const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
 };
 
@@ -84,6 +86,59 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
   }
 }
 
+// One (pixel P of the batch, 4 channels co..co+3) of a split-K conv: the tl.ksplit f32 partials
+// summed in split order onto the bias, the activation, and the split hi/lo (+ dense f32) store of
+// the kernels' own epilogue.  conv_m16_splitk_reduce runs it per thread; with tl.cnt the last
+// workgroup of a tile to finish its split runs it over the tile (splitk_arrive): same arithmetic,
+// same order, bit-identical outputs.
+__device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, const SplitConvGroup& g, int grp,
+                                                   const BigTiling& tl, int wsc, int64_t P, int co) {
+  floatx4 v = *(const floatx4*)(g.bias + co);
+  for (int sp = 0; sp < tl.ksplit; ++sp) {
+    const floatx4 a = *(const floatx4*)(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += a[e];
+  }
+  const int f = (int)(P / tl.hw), pp = (int)(P - (int64_t)f * tl.hw);
+  const int y = pp / s.w, x = pp - y * s.w;
+  const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;
+  const int64_t out_pc = split_piece_stride(s.out_planar, hp_out, wp_out);
+  char* d = (char*)g.out + (int64_t)f * hp_out * wp_out * s.cs_out * 4 +
+            ((int64_t)(y + s.pout) * wp_out + (x + s.pout)) * split_pixel_stride(s.out_planar, s.cs_out) +
+            (co >> 3) * 2 * out_pc + (co & 7) * 2;
+  u16x4g vh, vl;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (s.relu) v[e] = v[e] > 0.0f ? v[e] : 0.0f;
+    const __bf16 h16 = (__bf16)v[e];
+    const __bf16 l16v = (__bf16)(v[e] - (float)h16);
+    vh[e] = __builtin_bit_cast(unsigned short, h16);
+    vl[e] = __builtin_bit_cast(unsigned short, l16v);
+  }
+  *(u16x4g*)d = vh;
+  *(u16x4g*)(d + out_pc) = vl;
+  if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
+}
+
+// Split-K arrival (round 4: one frame's launches without a reduce launch).  Called by every thread
+// of a split's workgroup after its partial stores; returns true in the workgroup that arrives last
+// at counter *cnt (which it resets to zero for the next launch).  Ordering (MI355X_MICROARCH.md,
+// inter-workgroup visibility): every wave drains its stores, the workgroup barrier, then one lane's
+// agent-scope acq_rel counter update (release: the partials reach memory past this XCD's L2;
+// acquire: the last arriver's caches are invalidated), a barrier, then plain loads.  `flag` is any
+// 4 B of LDS no wave reads any more.
+__device__ __forceinline__ bool splitk_arrive(int32_t* cnt, int nsplit, volatile int* flag) {
+  wait_vmcnt<0>();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == nsplit - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
 
 // conv_m16.hip: launch conv_m16_bf16x3<7, npx, deep> on a raster tiling made by conv_big.hip (picks
 // the deep weight ring for small tiles; sets the kernels' LDS attribute on first use).

@@ -233,6 +233,14 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
           if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
         }
       }
+      // the tile's last split to finish sums all of them (no conv_m16_splitk_reduce launch)
+      if (tl.cnt && splitk_arrive(tl.cnt + (unit * tl.per_unit + widx), nsplit, (volatile int*)lds)) {
+        const int np = T.P1 - T.P0 + 1;
+        for (int i = threadIdx.x; i < np * (CW / 4); i += 512) {
+          const int P = T.P0 + i / (CW / 4), co = co0 + (i % (CW / 4)) * 4;
+          if (co < g.cout_store) splitk_reduce_item(s, g, grp, tl, wsc, P, co);
+        }
+      }
     } else {
       const int wp_out = s.w + 2 * s.pout;
       const int hp_out = s.h + 2 * s.pout;

@@ -19,6 +19,7 @@
 namespace op {
 
 constexpr int kMaxSubsetsLds = 2048;
+constexpr int kPeakScoreLds = 8192;  // grouping<false>: a frame's peak scores staged in LDS up to this count
 
 __device__ __forceinline__ double linspace_at(double start, double stop, int num, int i) {
   if (num == 1) return start;
@@ -521,6 +522,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   __shared__ double sc_lds[kRows][2];
   __shared__ int base[OP_N_JOINTS + 1];
   __shared__ int cnt[OP_N_JOINTS];
+  __shared__ float pk_lds[kBig ? 1 : kPeakScoreLds];  // peak scores by global peak id
   const int f = blockIdx.x;
   IdT (*ids)[OP_N_JOINTS];
   double (*sc)[2];
@@ -548,24 +550,49 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   __syncthreads();
   const int n_peaks = base[OP_N_JOINTS];
   int S = 0;
+  // round 4: no chain of dependent global loads per limb.  The frame's peak scores go to LDS in one
+  // pass (all loads in flight together), every limb's connection count is one lane's load, and a
+  // limb's first 64 connections (ids, score; one per lane, broadcast from registers) are fetched
+  // while the previous limb is processed.
+  const bool pk_lds_ok = !kBig && n_peaks <= kPeakScoreLds;
+  if (pk_lds_ok) {
+    for (int i = lane; i < n_peaks; i += 64) {
+      int j = 0;
+      while (base[j + 1] <= i) ++j;
+      pk_lds[i] = b.peak_score[((int64_t)f * OP_N_JOINTS + j) * b.maxp + (i - base[j])];
+    }
+  }
+  const int kc = lane < OP_N_LIMBS ? b.conn_cnt[(int64_t)f * OP_N_LIMBS + lane] : 0;
+  __syncthreads();
   auto pscore = [&](int joint, int id) -> double {
+    if (pk_lds_ok) return (double)pk_lds[id];
     return (double)b.peak_score[((int64_t)f * OP_N_JOINTS + joint) * b.maxp + (id - base[joint])];
   };
+  auto fetch = [&](int l, int cb, int& ia, int& ib, double& sc) {
+    const int K = __shfl(kc, l);
+    ia = 0;
+    ib = 0;
+    sc = 0.0;
+    if (cb + lane < K) {
+      const int64_t q = ((int64_t)f * OP_N_LIMBS + l) * b.maxp + cb + lane;
+      ia = b.conn_ab[2 * q];
+      ib = b.conn_ab[2 * q + 1];
+      sc = b.conn_score[q];
+    }
+  };
+  int nx_ia, nx_ib;
+  double nx_sc;
+  fetch(0, 0, nx_ia, nx_ib, nx_sc);
   for (int l = 0; l < OP_N_LIMBS && status == OP_OK; ++l) {
     const int ja = s.limbs[l][0], jb = s.limbs[l][1];
-    const int64_t fl = (int64_t)f * OP_N_LIMBS + l;
-    const int K = b.conn_cnt[fl];
-    // round 4: the limb's connections (ids, score, both peaks' scores) are fetched 64 at a time, one
-    // per lane, and broadcast from registers: the loop over connections no longer waits on a chain
-    // of dependent global loads per connection (one frame with 7 people: 74 -> ? us)
+    const int K = __shfl(kc, l);
+    int my_ia = nx_ia, my_ib = nx_ib;
+    double my_sc = nx_sc;
+    if (l + 1 < OP_N_LIMBS) fetch(l + 1, 0, nx_ia, nx_ib, nx_sc);
     for (int cb = 0; cb < K && status == OP_OK; cb += 64) {
-    int my_ia = 0, my_ib = 0;
-    double my_sc = 0.0, my_pa = 0.0, my_pb = 0.0;
+    if (cb > 0) fetch(l, cb, my_ia, my_ib, my_sc);
+    double my_pa = 0.0, my_pb = 0.0;
     if (cb + lane < K) {
-      const int64_t q = fl * b.maxp + cb + lane;
-      my_ia = b.conn_ab[2 * q];
-      my_ib = b.conn_ab[2 * q + 1];
-      my_sc = b.conn_score[q];
       my_pa = pscore(ja, my_ia);
       my_pb = pscore(jb, my_ib);
     }

@@ -231,15 +231,19 @@ struct PostRecord {
 // holds), copied aside on the device when the records are packed, so the owning rank can re-run
 // them after the next step has overwritten the batched buffers (op_comm_overflow*).
 struct KeepSlot {
-  float* maps = nullptr;
+  // kept frames are compacted into `slots` entries (OP_KEEP_FRAMES, default 8; advisor r03: sizing
+  // these for every frame of the pack cost GBs per slot at 1280x720), assigned by device counters
+  float* maps = nullptr;  // [slot][fstride] post-process input of frames over the batched caps
   size_t maps_cap = 0;  // bytes
-  double* res = nullptr;  // frames past max_persons: their batched result rows [frame][maxs][54 + 1]
+  double* res = nullptr;  // [slot][maxs][54 + 1] rows of frames past max_persons not in h_rows
   size_t res_cap = 0;
+  int slots = 0;
   int maxs = 0;
   int32_t* cnt = nullptr;
   size_t cnt_cap = 0;
   // n x kKeepHdr {status, n_peaks, n_persons, why: 0 whole record, 1 over the caps, 2 > max_persons,
-  // offset of the frame's rows in h_rows (doubles; -1: not there, read them from res)}
+  // where: why 1: its maps / cnt slot; why 2: >= 0 offset of its rows in h_rows (doubles), <= -2
+  // res slot -2 - where; -1: not kept (more such frames than slots: OP_ERR_CAPACITY on collection)}
   int32_t* d_hdr = nullptr;
   int32_t* h_hdr = nullptr;  // pinned copy, complete when the slot's gather is
   size_t hdr_cap = 0;
@@ -251,7 +255,7 @@ struct KeepSlot {
   double* d_rows_view = nullptr;  // the device's address of h_rows (hipHostGetDevicePointer)
   int64_t h_rows_cap = 0;  // doubles
   int64_t rows_cap_now = 0;  // of them, usable by the current pack (OP_KEEP_ROWS_AVG)
-  int32_t* d_rows_cnt = nullptr;
+  int32_t* d_rows_cnt = nullptr;  // [0] h_rows allocator, [1] maps slots, [2] res slots
   PostRecord rec{};
   int n = 0;
 };
@@ -752,14 +756,50 @@ static int conv2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int
 // Fused 1x1 pair per branch (conv5_4+conv5_5, Mconv6+Mconv7): in -> a (ReLU) -> b -> out, the
 // intermediate kept on chip (conv_head.hip).  Returns -1 when not taken (the caller then runs the
 // two convs through `mid`).  OP_HEAD_FUSED=0 disables it (A/B).
-static bool head_fused_on() {
-  static const bool off = getenv("OP_HEAD_FUSED") && atoi(getenv("OP_HEAD_FUSED")) == 0;
-  return !off;
+static bool head_fused_on() {  // read per forward (not cached): the parity tests A/B it in-process
+  const char* e = getenv("OP_HEAD_FUSED");
+  return !(e && atoi(e) == 0);
 }
 
 static int head2(op_ctx* c, const Act& in, int ci0, int ci1, const Act& out, int co0, int co1,
                  const PackedConv* a, const PackedConv* b, int st0, int st1, const Act* out32, int o32a, int o32b) {
-  if (!c->split || !head_fused_on()) return -1;
+  if (!head_fused_on()) return -1;
+  if (!c->split) {  // exact f32: conv_head_f32 (bit-identical to the two conv2 launches)
+    if (out32 || a[0].ks != 1 || b[0].ks != 1 || a[0].cop % 128 || a[0].cop != a[1].cop ||
+        b[0].cin_phys != a[0].cop || b[1].cin_phys != a[1].cop || b[0].cop != b[1].cop)
+      return -1;
+    HeadF32Shape s;
+    s.n = c->gn;
+    s.h = out.h;
+    s.w = out.w;
+    s.pin = in.pad;
+    s.cs_in = in.cs;
+    s.pout = out.pad;
+    s.cs_out = out.cs;
+    s.c8 = a[0].cin_phys / 8;
+    s.co1 = a[0].cop;
+    s.groups = 2;
+    HeadF32Group g[2];
+    const int cis[2] = {ci0, ci1}, cos[2] = {co0, co1}, sts[2] = {st0, st1};
+    for (int i = 0; i < 2; ++i) {
+      g[i].in = in.p + cis[i];
+      g[i].w1 = a[i].w;
+      g[i].b1 = a[i].b;
+      g[i].cop1 = a[i].cop;
+      g[i].w2 = b[i].w;
+      g[i].b2 = b[i].b;
+      g[i].cop2 = b[i].cop;
+      g[i].out = out.p + cos[i];
+      g[i].cout_store = sts[i];
+    }
+    double fl = 0, by = 0;
+    for (int i = 0; i < 2; ++i) {
+      conv_work(c, out, a[i], &fl, &by);
+      conv_work(c, out, b[i], &fl, &by);
+    }
+    const int rc = profiled(c, 2, fl, by, [&] { return launch_conv_head_f32(s, g, c->stream); });
+    return rc ? rc : 0;
+  }
   HeadShape s;
   s.n = c->gn;
   s.h = out.h;
@@ -2279,7 +2319,7 @@ __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, in
                                                     int32_t* __restrict__ rows_cnt) {
   const int i = blockIdx.x;
   const int f = first + i;
-  if (rows_cnt && i == 0 && threadIdx.x == 0) *rows_cnt = 0;  // keep_overflow's row allocator
+  if (rows_cnt && i == 0 && threadIdx.x < 3) rows_cnt[threadIdx.x] = 0;  // keep_overflow's allocators
   char* r = out + (int64_t)i * rec_bytes;
   const int status = b.res_hdr[4 * f];
   const int persons = status == OP_OK ? b.res_hdr[4 * f + 2] : 0;
@@ -2310,7 +2350,7 @@ __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, i
                                                      int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
                                                      double* __restrict__ res, int32_t* __restrict__ hdr,
                                                      double* __restrict__ h_rows, int64_t h_rows_cap,
-                                                     int32_t* __restrict__ rows_cnt) {
+                                                     int32_t* __restrict__ rows_cnt, int slots) {
   const int i = blockIdx.x;
   const int f = first + i;
   const int status = b.res_hdr[4 * f];
@@ -2319,9 +2359,16 @@ __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, i
   __shared__ int off_s;
   if (threadIdx.x == 0) {
     int off = -1;
-    if (why == 2) {  // rows -> page-locked host memory, if the slot's capacity holds them
+    if (why == 2) {  // rows -> page-locked host memory, if the slot's capacity holds them, else a res slot
       const int o = atomicAdd(rows_cnt, persons * 55);
       if ((int64_t)o + persons * 55 <= h_rows_cap) off = o;
+      else {
+        const int sl = atomicAdd(rows_cnt + 2, 1);
+        if (sl < slots) off = -2 - sl;
+      }
+    } else if (why == 1 && src) {
+      const int sl = atomicAdd(rows_cnt + 1, 1);
+      if (sl < slots) off = sl;
     }
     off_s = off;
     hdr[kKeepHdr * i] = status;
@@ -2331,20 +2378,21 @@ __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, i
     hdr[kKeepHdr * i + 4] = off;
   }
   __syncthreads();
+  const int off = off_s;
   if (why == 2) {
+    if (off == -1) return;
     const double* ps = b.res_poses + (int64_t)f * b.maxs * 54;
     const double* ss = b.res_scores + (int64_t)f * b.maxs;
-    const int off = off_s;
-    double* d = off >= 0 ? h_rows + off : res + (int64_t)i * b.maxs * 55;
+    double* d = off >= 0 ? h_rows + off : res + (int64_t)(-2 - off) * b.maxs * 55;
     const int64_t sc = off >= 0 ? (int64_t)persons * 54 : (int64_t)b.maxs * 54;
     for (int e = threadIdx.x; e < persons * 54; e += 256) d[e] = ps[e];
     for (int e = threadIdx.x; e < persons; e += 256) d[sc + e] = ss[e];
     return;
   }
-  if (why != 1 || !src) return;
-  if (threadIdx.x < OP_N_JOINTS) cnt[i * OP_N_JOINTS + threadIdx.x] = b.peak_cnt[f * OP_N_JOINTS + threadIdx.x];
+  if (why != 1 || !src || off < 0) return;
+  if (threadIdx.x < OP_N_JOINTS) cnt[off * OP_N_JOINTS + threadIdx.x] = b.peak_cnt[f * OP_N_JOINTS + threadIdx.x];
   const float* s = src + (int64_t)f * fstride;
-  float* d = dst + (int64_t)i * fstride;
+  float* d = dst + (int64_t)off * fstride;
   for (int64_t e = threadIdx.x; e < fstride; e += 256) d[e] = s[e];
 }
 
@@ -2360,7 +2408,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
   int32_t* rows_cnt = nullptr;
   if (keep_slot >= 0) {
     KeepSlot& k = c->keep[keep_slot];
-    if (!k.d_rows_cnt) OP_HIP_CHECK(hipMalloc((void**)&k.d_rows_cnt, sizeof(int32_t)));
+    if (!k.d_rows_cnt) OP_HIP_CHECK(hipMalloc((void**)&k.d_rows_cnt, 3 * sizeof(int32_t)));
     // page-locked rows for frames past max_persons: 256 persons per frame on average (the rest,
     // if ever, are read from the device copy in res; OP_KEEP_ROWS_AVG overrides the 256, 0 sends
     // every such frame through the device copy -- a test aid)
@@ -2392,11 +2440,13 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     const PostRecord& r = c->post_rec;
     const float* src = r.kind == 1 ? r.low.base : r.kind == 2 ? r.full : nullptr;
     const int64_t fstride = r.kind == 1 ? r.low.fstride : r.fstride;
+    const char* kf_env = getenv("OP_KEEP_FRAMES");
+    k.slots = std::min(n, kf_env ? std::max(1, atoi(kf_env)) : 8);
     if (src) {
-      RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)n * fstride * 4, "keep_maps"));
-      RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)n * OP_N_JOINTS * 4, "keep_cnt"));
+      RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)k.slots * fstride * 4, "keep_maps"));
+      RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)k.slots * OP_N_JOINTS * 4, "keep_cnt"));
     }
-    RC(grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)n * c->pb.maxs * 55 * 8, "keep_res"));
+    RC(grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)k.slots * c->pb.maxs * 55 * 8, "keep_res"));
     k.maxs = c->pb.maxs;
     const size_t hb = (size_t)n * kKeepHdr * 4;
     if (hb > k.hdr_cap) {
@@ -2412,7 +2462,7 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     }
     RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
       hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                         k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt);
+                         k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt, k.slots);
       OP_AFTER_LAUNCH("keep_overflow", c->stream);
       return OP_OK;
     }));
@@ -2478,7 +2528,11 @@ int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* score
       memcpy(scores, h + (size_t)p * 54, (size_t)p * 8);
       return OP_OK;
     }
-    const double* d = k.res + (size_t)frame * k.maxs * 55;
+    if (hd[4] == -1) {
+      set_error("kept result: more frames past max_persons than keep slots (OP_KEEP_FRAMES) in this gather");
+      return OP_ERR_CAPACITY;
+    }
+    const double* d = k.res + (size_t)(-2 - hd[4]) * k.maxs * 55;
     OP_HIP_CHECK(hipMemcpy(poses, d, (size_t)p * 54 * 8, hipMemcpyDeviceToHost));
     OP_HIP_CHECK(hipMemcpy(scores, d + (size_t)k.maxs * 54, (size_t)p * 8, hipMemcpyDeviceToHost));
     return OP_OK;
@@ -2487,8 +2541,12 @@ int ctx_kept_result(op_ctx* c, int slot, int frame, double* poses, double* score
     set_error("kept result: no recorded post-process input for this slot");
     return OP_ERR_STATE;
   }
+  if (hd[4] < 0) {
+    set_error("kept result: more frames over the post-process caps than keep slots (OP_KEEP_FRAMES) in this gather");
+    return OP_ERR_CAPACITY;
+  }
   PostBuffers* B = nullptr;
-  RC(rerun_big_rec(c, k.rec, frame, k.cnt + (size_t)frame * OP_N_JOINTS, &B));
+  RC(rerun_big_rec(c, k.rec, hd[4], k.cnt + (size_t)hd[4] * OP_N_JOINTS, &B));
   return read_big(B, poses, scores, cap, res);
 }
 

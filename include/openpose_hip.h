@@ -297,6 +297,7 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_7X7_TIGHT 24   /* conv_m16 7x7 launches with the tight halo pitch w + 6 (wide maps) */
 #define OP_CENSUS_CUBIC_FUSED 25 /* detect_precise map resizes as one fused pass (resize_cubic_fused_mean) */
 #define OP_CENSUS_CUBIC_TWO_PASS 26 /* ... as the two-pass path (padded-size maps in HBM) */
+#define OP_CENSUS_SPLITK_INKERNEL 27 /* split-K launches (7x7 or 3x3) finished by their last split, no reduce launch */
 #define OP_CENSUS_SLOTS 32
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

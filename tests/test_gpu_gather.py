@@ -163,3 +163,34 @@ def test_every_frame_reaches_rank0_whole(ctx, rows_avg, monkeypatch):
     finally:
         ctx.use_staged_maps(False)
         g.close()
+
+
+def test_keep_slots_are_bounded(ctx, monkeypatch):
+    """Advisor r03 (low): the keep buffers hold OP_KEEP_FRAMES (default 8) compacted frames, not every
+    frame of the pack.  With OP_KEEP_ROWS_AVG=0 every frame past max_persons goes through a device
+    keep slot; with OP_KEEP_FRAMES=1 the second such frame of one gather has no slot, and collecting
+    the step fails loudly (OP_ERR_CAPACITY) instead of returning another frame's rows."""
+    monkeypatch.setenv("OP_KEEP_ROWS_AVG", "0")
+    monkeypatch.setenv("OP_KEEP_FRAMES", "1")
+    F = pkg_module("frames")
+    six = load_golden("six_people")
+    six_maps = np.concatenate([six["paf_low"], six["heat_low"]])
+    n = 2
+    ctx.stage_frames(np.zeros((n, 368, 368, 3), np.uint8))
+    g = F.RcclGather(ctx, F.SocketTransport(0, 1), max_persons=MAXP, timeout=60)
+    try:
+        ctx.stage_maps(np.stack([six_maps, six_maps]))  # both frames hold more persons than MAXP
+        ctx.use_staged_maps(True)
+        ctx.run_staged()
+        g.submit(0, n, 0, 1)
+        with pytest.raises(RuntimeError, match="keep slots"):
+            g.wait(raw=True)
+        monkeypatch.setenv("OP_KEEP_FRAMES", "2")  # read per pack: both frames kept again
+        ctx.run_staged()
+        g.submit(0, n, 0, 1)
+        raw, ovf = g.wait(raw=True)
+        assert sorted(r[0] for r in ovf) == [0, 1]
+        assert F.count_persons(raw, MAXP, ovf)[1] == 0
+    finally:
+        ctx.use_staged_maps(False)
+        g.close()

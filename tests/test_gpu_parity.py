@@ -179,6 +179,41 @@ def test_forward_7x7_tile_sizes_agree(ctx):
         assert err <= 1e-4 * mag, (i, err, mag)  # 10x inside the 1e-3 parity tolerance
 
 
+def test_splitk_in_kernel_equals_reduce_launch(ctx, lib, monkeypatch):
+    """Round 4: a split-K launch (one frame's 7x7 and 3x3 layers) finishes in the conv kernel -- the
+    last split of each tile to arrive (agent-scope acq_rel counter) sums the partials in split order
+    (conv_big.hpp splitk_arrive / splitk_reduce_item) -- instead of in a conv_m16_splitk_reduce
+    launch.  Same arithmetic in the same order: maps BIT-IDENTICAL to OP_SPLITK_INKERNEL=0, eager
+    and under hipGraph replay (the counters are reset by their last arrivals)."""
+    rng = np.random.default_rng(27)
+    x = rng.uniform(-0.5, 0.5, (1, 3, 368, 368)).astype(np.float32)
+    lib.conv_census(reset=True)
+    fused = ctx.forward(x)
+    cen = lib.conv_census(reset=True)
+    assert cen["splitk_inkernel"] > 0 and cen["7x7_splitk"] > 0 and cen["3x3_splitk"] > 0, cen
+    again = ctx.forward(x)  # counters back at zero after every launch
+    lib.conv_census(reset=True)
+    monkeypatch.setenv("OP_SPLITK_INKERNEL", "0")
+    plain = ctx.forward(x)
+    cen = lib.conv_census(reset=True)
+    monkeypatch.delenv("OP_SPLITK_INKERNEL")
+    assert cen["splitk_inkernel"] == 0 and cen["7x7_splitk"] > 0, cen
+    for a, b, c in zip(fused, again, plain):
+        assert np.array_equal(a, b) and np.array_equal(a, c), float(np.abs(a - c).max())
+    # staged frames through the captured graph (in-kernel path) vs eager with reduce launches
+    frames = rng.integers(0, 256, (1, 368, 368, 3), dtype=np.uint8)
+    monkeypatch.setenv("OP_SPLITK_INKERNEL", "0")
+    want = ctx.detect(frames[0])
+    monkeypatch.delenv("OP_SPLITK_INKERNEL")
+    ctx.stage_frames(frames)
+    for graph in (False, True, True):
+        ctx.run_staged(graph=graph)
+        ctx.synchronize()
+        p, s, r = ctx.fetch_result(0)
+        assert r.n_peaks == want[2].n_peaks
+        assert np.array_equal(p, want[0]) and np.array_equal(s, want[1])
+
+
 def test_forward_precisions_agree(ctx, rand_weights):
     """bf16x3 vs exact-f32 MFMA on a 720p-shaped input (656x368), batch 2."""
     rng = np.random.default_rng(2)
@@ -190,6 +225,30 @@ def test_forward_precisions_agree(ctx, rand_weights):
     err = max(float(np.abs(p32 - p16).max()), float(np.abs(h32 - h16).max()))
     print("bf16x3 vs fp32 at 656x368: %.3g" % err)
     assert err <= FWD_TOL
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
+def test_fused_heads_equal_two_launches(ctx, prec, monkeypatch):
+    """Each branch's closing 1x1 pair (conv5_4 + conv5_5, Mconv6 + Mconv7; CocoPoseNet.py:162-165,
+    181-184) runs as one launch with the intermediate on chip (fp32: conv.hip conv_head_f32; bf16x3:
+    conv_head.hip).  The fp32 kernel contracts both layers in the two-launch kernel's order, so every
+    stage's maps are BIT-IDENTICAL with OP_HEAD_FUSED=0; the bf16x3 kernel re-splits the
+    intermediate on chip and is held to 1e-4 x the map magnitude."""
+    rng = np.random.default_rng(21)
+    x = rng.uniform(-0.5, 0.5, (2, 3, 184, 248)).astype(np.float32)
+    ctx.set_precision(prec)
+    try:
+        fused = ctx.forward(x)
+        monkeypatch.setenv("OP_HEAD_FUSED", "0")
+        plain = ctx.forward(x)
+        monkeypatch.delenv("OP_HEAD_FUSED")
+    finally:
+        ctx.set_precision("bf16x3")
+    for a, b in zip(fused, plain):
+        if prec == "fp32":
+            assert np.array_equal(a, b), float(np.abs(a - b).max())
+        else:
+            assert float(np.abs(a - b).max()) <= 1e-4 * max(1.0, float(np.abs(b).max()))
 
 
 def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
