@@ -453,11 +453,15 @@ static float* splitk_ws(hipStream_t st, size_t floats) {
   return p;
 }
 
-// The stream's arrival counters when a launch of `tiles` (weight set, pixel tile) pairs can finish
-// its split-K in the conv kernel (OP_SPLITK_INKERNEL=0: always the reduce launch, an A/B aid).
+// The stream's arrival counters when a launch of `tiles` (weight set, pixel tile) pairs finishes
+// its split-K in the conv kernel -- OFF by default, OP_SPLITK_INKERNEL=1 selects it: one frame's
+// 368x368 call measured 3.03 ms per frame against 1.95 with the reduce launches
+// (profiles/r04/ab_r04l_splitk_inkernel_sc1.log).  The last arriver of a tile reads all S partials
+// of the tile alone: 22-44 CUs pull the launch's 17 MB of partials at one CU's bandwidth each, where
+// conv_m16_splitk_reduce spreads the same bytes over the whole chip in 6.4 us.
 static int32_t* splitk_counters(hipStream_t st, int64_t tiles) {
   const char* e = getenv("OP_SPLITK_INKERNEL");  // read per launch: the parity test A/Bs it in-process
-  if ((e && atoi(e) == 0) || tiles > kSplitkCounters) return nullptr;
+  if (!(e && atoi(e) == 1) || tiles > kSplitkCounters) return nullptr;
   std::lock_guard<std::mutex> lk(g_ws_mu);
   auto it = g_ws.find(st);
   return it == g_ws.end() ? nullptr : it->second.cnt;
@@ -502,7 +506,7 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
   if (i >= (int64_t)tl.total * q) return;
   const int P = (int)(i / q), co = (int)(i - (int64_t)P * q) * 4;
   if (co >= g.cout_store) return;
-  splitk_reduce_item(s, g, grp, tl, max(g0.cop, g1.cop), P, co);
+  splitk_reduce_item<false>(s, g, grp, tl, max(g0.cop, g1.cop), P, co);
 }
 
 // Split-K partials of a conv with the fused 2x2 max-pool (round 4: pooled 3x3 launches that fill

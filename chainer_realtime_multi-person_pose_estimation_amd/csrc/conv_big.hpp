@@ -86,16 +86,50 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
   }
 }
 
+// Split-K hand-off inside a launch (round 4 experiment, opt-in OP_SPLITK_INKERNEL=1: slower, see
+// splitk_counters in conv_big.hip): the split workgroups of a tile
+// write their f32 partials WRITE-THROUGH (`sc1`: 8-B agent-scope relaxed stores, no L2 copy), each
+// storing wave drains them (vmcnt(0)), the workgroup barrier, then ONE lane adds to the tile's
+// counter (agent-scope relaxed atomic); the workgroup whose add returns nsplit - 1 arrived last and
+// reads every partial with `sc1` loads (bypassing its CU's L1) -- the hand-off form of
+// MI355X_MICROARCH.md's visibility table (row 1: no release fence, no acquire).  An agent-scope
+// release fence in its place writes back the whole XCD L2 per workgroup: measured 1.96 -> 3.04 ms
+// per frame (profiles/r04/ab_r04k_splitk_inkernel_release_fence.log).
+typedef float floatx2g __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+__device__ __forceinline__ void store_partial_sc1(float* p, const floatx4& v) {
+  gu64_t* q = (gu64_t*)p;
+  __hip_atomic_store(q, __builtin_bit_cast(unsigned long long, floatx2g{v[0], v[1]}), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, __builtin_bit_cast(unsigned long long, floatx2g{v[2], v[3]}), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool SC1>
+__device__ __forceinline__ floatx4 load_partial(const float* p) {
+  if constexpr (SC1) {
+    gu64_t* q = (gu64_t*)p;
+    const floatx2g a = __builtin_bit_cast(floatx2g, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const floatx2g b = __builtin_bit_cast(floatx2g, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return floatx4{a[0], a[1], b[0], b[1]};
+  } else {
+    return *(const floatx4*)p;
+  }
+}
+
 // One (pixel P of the batch, 4 channels co..co+3) of a split-K conv: the tl.ksplit f32 partials
 // summed in split order onto the bias, the activation, and the split hi/lo (+ dense f32) store of
-// the kernels' own epilogue.  conv_m16_splitk_reduce runs it per thread; with tl.cnt the last
-// workgroup of a tile to finish its split runs it over the tile (splitk_arrive): same arithmetic,
-// same order, bit-identical outputs.
+// the kernels' own epilogue.  conv_m16_splitk_reduce runs it per thread (SC1 = false: a launch
+// boundary orders it after the conv); with tl.cnt the tile's last split runs it over the tile
+// (SC1: the partials handed off inside the launch).  Same arithmetic, same order: bit-identical.
+template <bool SC1>
 __device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, const SplitConvGroup& g, int grp,
                                                    const BigTiling& tl, int wsc, int64_t P, int co) {
   floatx4 v = *(const floatx4*)(g.bias + co);
   for (int sp = 0; sp < tl.ksplit; ++sp) {
-    const floatx4 a = *(const floatx4*)(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+    const floatx4 a = load_partial<SC1>(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] += a[e];
   }
@@ -120,20 +154,24 @@ __device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, cons
   if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
 }
 
-// Split-K arrival (round 4: one frame's launches without a reduce launch).  Called by every thread
-// of a split's workgroup after its partial stores; returns true in the workgroup that arrives last
-// at counter *cnt (which it resets to zero for the next launch).  Ordering (MI355X_MICROARCH.md,
-// inter-workgroup visibility): every wave drains its stores, the workgroup barrier, then one lane's
-// agent-scope acq_rel counter update (release: the partials reach memory past this XCD's L2;
-// acquire: the last arriver's caches are invalidated), a barrier, then plain loads.  `flag` is any
-// 4 B of LDS no wave reads any more.
-__device__ __forceinline__ bool splitk_arrive(int32_t* cnt, int nsplit, volatile int* flag) {
+// Called by every thread of a split's workgroup after its sc1 partial stores; true in the workgroup
+// that arrives last at *cnt (which it resets to zero for the next launch).  ACQUIRE: that workgroup
+// also runs one agent-scope acquire before its loads (kernels with more than one workgroup per CU,
+// outside the measured row).  `lds_word`: 4 B of LDS no wave reads any more.
+template <bool ACQUIRE>
+__device__ __forceinline__ bool splitk_arrive(int32_t* cnt, int nsplit, char* lds_word) {
+  __attribute__((address_space(3))) volatile int* flag = (__attribute__((address_space(3))) volatile int*)lds_word;
   wait_vmcnt<0>();
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    gi32_t* c = (gi32_t*)cnt;
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = old == nsplit - 1;
-    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ACQUIRE && last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      wait_vmcnt<0>();
+    }
     *flag = last ? 1 : 0;
   }
   __syncthreads();

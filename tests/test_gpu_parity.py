@@ -180,13 +180,15 @@ def test_forward_7x7_tile_sizes_agree(ctx):
 
 
 def test_splitk_in_kernel_equals_reduce_launch(ctx, lib, monkeypatch):
-    """Round 4: a split-K launch (one frame's 7x7 and 3x3 layers) finishes in the conv kernel -- the
-    last split of each tile to arrive (agent-scope acq_rel counter) sums the partials in split order
-    (conv_big.hpp splitk_arrive / splitk_reduce_item) -- instead of in a conv_m16_splitk_reduce
-    launch.  Same arithmetic in the same order: maps BIT-IDENTICAL to OP_SPLITK_INKERNEL=0, eager
-    and under hipGraph replay (the counters are reset by their last arrivals)."""
+    """Round 4 experiment (opt-in OP_SPLITK_INKERNEL=1, measured slower): a split-K launch (one
+    frame's 7x7 and 3x3 layers) finishes in the conv kernel -- the last split of each tile to arrive
+    (sc1 partials, agent-scope counter) sums the partials in split order (conv_big.hpp splitk_arrive
+    / splitk_reduce_item) -- instead of in a conv_m16_splitk_reduce launch.  Same arithmetic in the
+    same order: maps BIT-IDENTICAL to the default, eager and under hipGraph replay (the counters are
+    reset by their last arrivals)."""
     rng = np.random.default_rng(27)
     x = rng.uniform(-0.5, 0.5, (1, 3, 368, 368)).astype(np.float32)
+    monkeypatch.setenv("OP_SPLITK_INKERNEL", "1")
     lib.conv_census(reset=True)
     fused = ctx.forward(x)
     cen = lib.conv_census(reset=True)
@@ -204,7 +206,7 @@ def test_splitk_in_kernel_equals_reduce_launch(ctx, lib, monkeypatch):
     frames = rng.integers(0, 256, (1, 368, 368, 3), dtype=np.uint8)
     monkeypatch.setenv("OP_SPLITK_INKERNEL", "0")
     want = ctx.detect(frames[0])
-    monkeypatch.delenv("OP_SPLITK_INKERNEL")
+    monkeypatch.setenv("OP_SPLITK_INKERNEL", "1")
     ctx.stage_frames(frames)
     for graph in (False, True, True):
         ctx.run_staged(graph=graph)
@@ -212,6 +214,7 @@ def test_splitk_in_kernel_equals_reduce_launch(ctx, lib, monkeypatch):
         p, s, r = ctx.fetch_result(0)
         assert r.n_peaks == want[2].n_peaks
         assert np.array_equal(p, want[0]) and np.array_equal(s, want[1])
+    monkeypatch.delenv("OP_SPLITK_INKERNEL")
 
 
 def test_forward_precisions_agree(ctx, rand_weights):
