@@ -173,15 +173,26 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
     for (int c = cb0; c < cb1; ++c) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#if M16_PROBE_NOHALO  // timing probe only (wrong results): the halo is loaded for the first chunk only
+      if (c == cb0) issue_halo(c, T);
+#else
       issue_halo(c, T);
+#endif
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       bf16x8g ah[4], al[4];
+#if M16_PROBE_NOPAD  // timing probe only (wrong results): the padding pair of the odd 49th tap skipped
+      constexpr int kPairsEnd = KSQ - 1;
+#else
+      constexpr int kPairsEnd = KSQP;
+#endif
 #pragma unroll 1
-      for (int t = 0; t < KSQP; t += 2, it += 2) {
+      for (int t = 0; t < kPairsEnd; t += 2, it += 2) {
         wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
+#if !M16_PROBE_NOBAR  // timing probe only (racy ring): no per-pair barrier
         __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
+#endif
         asm volatile("" ::: "memory");
         stage_w(it + 2 * AHEAD);
         stage_w(it + 2 * AHEAD + 1);
