@@ -16,7 +16,7 @@
 // 4 (w / 2) .. + 3): a wave's per-step A fragments (read from L2) feed 8 pixel blocks, where 64
 // channels x 4 blocks read every A fragment in all four waves (conv1_pair -2.8 %; 16 x 16: +1.4 %).  LDS 48 KiB:
 // three workgroups per CU, so one's conv1_1 (VALU) phase overlaps the others' MFMA phases.
-#include "common.hpp"
+#include "conv_big.hpp"  // split_pair_swap
 #include "cvlinear.hpp"
 
 namespace op {
@@ -35,6 +35,9 @@ constexpr int kP1Plane = (kP1Slots * 16 + 255) / 256 * 256;  // (no measurable c
 [[maybe_unused]] constexpr int kP1Items = 384;                      // conv1_1 work items per 16-channel group (6 waves)
 #ifndef C1P_COW
 #define C1P_COW 32
+#endif
+#ifndef C1P_SWAP
+#define C1P_SWAP 1  // conv1_1's split stores as one ds_write_b128 per lane after a row swap (0: 2 x 8 B)
 #endif
 #ifndef C1P_MFMA11
 #define C1P_MFMA11 1  // conv1_1 on MFMA (0: the f32 VALU form, in the CPU oracle's FMA order)
@@ -177,6 +180,22 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
           d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11h[cb], bh, d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11h[cb], bl, d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a11l[cb], bh, d, 0, 0, 0);
+#if C1P_SWAP
+          // round 4: rows kg, kg ^ 1 (channels 4 kg .. +3 and the other half of the same 8-channel
+          // piece) swap halves with v_permlane16_swap (split_pair_swap: VALU, no LDS traffic), so
+          // the even row stores the piece's 16 hi bytes and the odd row its 16 lo bytes, one
+          // ds_write_b128 each: 8 lanes of a row = 128 contiguous bytes, conflict-free, where the
+          // two 8-B stores per lane were 2-way conflicted (ds_write_b64 banks 16 lanes at once)
+          // (conv1_2's zero padding outside the image)
+          floatx4 dm, v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dm[e] = inside ? d[e] : 0.0f;
+          uint32_t own[4], wv[4];
+          split_pair_swap(dm, floatx4{0.f, 0.f, 0.f, 0.f}, 1, v, own, wv);
+          if (sl < kP1Slots)
+            *(uint4*)(halo + (cb * 4 + 2 * (kg >> 1) + (kg & 1)) * kP1Plane + sl * 16) =
+                make_uint4(wv[0], wv[1], wv[2], wv[3]);
+#else
           // lane: channels 16 cb + 4 kg .. + 3 of slot sl -> 8 bytes of the (chunk cb, half kg / 2)
           // hi and lo planes (conv1_2's zero padding outside the image)
           u16x4p hv, lv;
@@ -192,6 +211,7 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
             *(u16x4p*)dst = hv;
             *(u16x4p*)(dst + kP1Plane) = lv;
           }
+#endif
         }
       }
     }

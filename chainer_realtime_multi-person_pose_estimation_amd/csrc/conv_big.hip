@@ -526,15 +526,25 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce_pool(SplitConvShap
   const int yo = pp / wo, xo = pp - yo * wo;
   const floatx4 bv = *(const floatx4*)(g.bias + co);
   floatx4 m = {0.f, 0.f, 0.f, 0.f};
+  // all 4 x ksplit partials loaded before the first add (splitk_reduce_item); split order kept
+  constexpr int kMaxPoolSplit = 8;
+  floatx4 part[4][kMaxPoolSplit];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t P = ((int64_t)f * s.h + 2 * yo + (k >> 1)) * s.w + 2 * xo + (k & 1);
-    floatx4 v = bv;
-    for (int sp = 0; sp < tl.ksplit; ++sp) {
-      const floatx4 a = *(const floatx4*)(tl.ws + ((int64_t)sp * tl.total + P) * g.cop + co);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += a[e];
-    }
+    for (int sp = 0; sp < kMaxPoolSplit; ++sp)
+      if (sp < tl.ksplit) part[k][sp] = *(const floatx4*)(tl.ws + ((int64_t)sp * tl.total + P) * g.cop + co);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    floatx4 v = bv;
+#pragma unroll
+    for (int sp = 0; sp < kMaxPoolSplit; ++sp)
+      if (sp < tl.ksplit) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += part[k][sp][e];
+      }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float fv = v[e];
@@ -777,6 +787,7 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
           S = cand;
           break;
         }
+    if (S > (pool ? 8 : kMaxSplitK)) S = 1;  // the reduce kernels' unrolled partial loads
     if (S > 1) {
       int cop_max = g[0].cop;
       if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
@@ -995,6 +1006,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       tl.ksplit = 1;
       tl.ws = nullptr;
       tl.cnt = nullptr;
+      if (S > kMaxSplitK) S = 1;  // the reduce's unrolled partial loads
       if (s.splitk && S > 1) {
         float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
         if (ws) {

@@ -124,15 +124,26 @@ __device__ __forceinline__ floatx4 load_partial(const float* p) {
 // the kernels' own epilogue.  conv_m16_splitk_reduce runs it per thread (SC1 = false: a launch
 // boundary orders it after the conv); with tl.cnt the tile's last split runs it over the tile
 // (SC1: the partials handed off inside the launch).  Same arithmetic, same order: bit-identical.
+// Round 4: every partial is loaded before the first add (a predicated, fully unrolled loop over at
+// most kMaxSplitK splits), so a thread waits for memory once instead of once per split (the
+// launch's 8 dependent load latencies were most of a one-frame reduce's 6.4 us); the adds keep
+// the split order.
+constexpr int kMaxSplitK = 16;
 template <bool SC1>
 __device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, const SplitConvGroup& g, int grp,
                                                    const BigTiling& tl, int wsc, int64_t P, int co) {
-  floatx4 v = *(const floatx4*)(g.bias + co);
-  for (int sp = 0; sp < tl.ksplit; ++sp) {
-    const floatx4 a = load_partial<SC1>(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+  floatx4 part[kMaxSplitK];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] += a[e];
-  }
+  for (int sp = 0; sp < kMaxSplitK; ++sp)
+    if (sp < tl.ksplit)
+      part[sp] = load_partial<SC1>(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+  floatx4 v = *(const floatx4*)(g.bias + co);
+#pragma unroll
+  for (int sp = 0; sp < kMaxSplitK; ++sp)
+    if (sp < tl.ksplit) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += part[sp][e];
+    }
   const int f = (int)(P / tl.hw), pp = (int)(P - (int64_t)f * tl.hw);
   const int y = pp / s.w, x = pp - y * s.w;
   const int wp_out = s.w + 2 * s.pout, hp_out = s.h + 2 * s.pout;

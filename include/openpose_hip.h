@@ -343,7 +343,10 @@ int op_comm_wait(op_comm* comm, double timeout_s, const void** records, int32_t*
  * op_fetch_result would have given) and a frame past max_persons kept its complete result rows
  * (copied out as they are) -- so both are exact even after later steps have run; the host ships
  * them to rank 0 (frames.py: TCP).  Valid until the next op_comm_gather_results, which packs into
- * that gather's slot (after it, both calls return OP_ERR_STATE until the next op_comm_wait). */
+ * that gather's slot (after it, both calls return OP_ERR_STATE until the next op_comm_wait).
+ * Device keep space per slot: OP_KEEP_FRAMES (env, default 8) frames of each kind, compacted (rows
+ * past max_persons go to page-locked memory first, OP_KEEP_ROWS_AVG); a frame beyond that has no
+ * copy and op_comm_overflow_result returns OP_ERR_CAPACITY for it. */
 int op_comm_overflow(op_comm* comm, op_ctx* ctx, int32_t* frames, int32_t* reasons, int32_t cap, int32_t* count);
 int op_comm_overflow_result(op_comm* comm, op_ctx* ctx, int32_t frame, double* poses, double* scores, int32_t cap,
                             op_frame_result* res);
