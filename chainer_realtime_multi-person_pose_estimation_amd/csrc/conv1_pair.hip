@@ -37,7 +37,10 @@ constexpr int kP1Plane = (kP1Slots * 16 + 255) / 256 * 256;  // (no measurable c
 #define C1P_COW 32
 #endif
 #ifndef C1P_SWAP
-#define C1P_SWAP 1  // conv1_1's split stores as one ds_write_b128 per lane after a row swap (0: 2 x 8 B)
+// 1: conv1_1's split stores as one ds_write_b128 per lane after a permlane16 row swap -- LDS
+// conflicts 0.66 -> 0.28 per instruction, but neutral to slower (conv3x3 42.60 vs 42.56 ms per
+// 232-frame step, 5-round A/B, profiles/r04/ab_r04s_*.log): off
+#define C1P_SWAP 0
 #endif
 #ifndef C1P_MFMA11
 #define C1P_MFMA11 1  // conv1_1 on MFMA (0: the f32 VALU form, in the CPU oracle's FMA order)
