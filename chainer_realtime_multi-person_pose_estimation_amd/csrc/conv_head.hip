@@ -44,17 +44,24 @@ __device__ __forceinline__ floatx4 mfma3(const bf16x8h& ah, const bf16x8h& al, c
   return acc;
 }
 
-// PXB (round 4): pixel blocks of 64 per workgroup -- 2 on large launches, so each workgroup's
-// weight fetch from L2 (W1: 64 KiB per 128-channel chunk) feeds twice the pixels.
-template <int NB2, bool ONE, int PXB = 1>
-__global__ __launch_bounds__(256, ONE ? 4 / PXB : 2 / PXB) void conv_head_bf16x3(HeadShape s, HeadGroup g0, HeadGroup g1,
+// PXB (round 4, opt-in OP_HEAD_PX=128, measured slower): pixel blocks of 64 per workgroup.
+// TPW (round 4, opt-in OP_HEAD_TPW, measured slower): 64-px tiles per workgroup, one after the other.  Mconv6 + Mconv7 (ONE) has a
+// single 128-channel chunk, so a wave's GEMM1 weight fragments (64 KiB per workgroup, re-read from
+// L2 by every workgroup: ~1 GB per 232-frame launch) are loaded once for TPW tiles.
+template <int NB2, bool ONE, int PXB = 1, int TPW = 1>
+#ifndef HEAD_TPW_OCC
+#define HEAD_TPW_OCC 3  // workgroups per CU the TPW > 1 forms are built for (a1 stays live across tiles)
+#endif
+__global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 / PXB) void conv_head_bf16x3(HeadShape s, HeadGroup g0,
+                                                                                                  HeadGroup g1,
                                                                                   int32_t per_group) {
   constexpr int CI = 128;  // both pairs read 128 channels per branch
   constexpr int kPx = kHeadPx * PXB;
+  static_assert(TPW == 1 || ONE, "several tiles per workgroup keep one chunk's weights");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int grp = blockIdx.x >= (unsigned)per_group ? 1 : 0;
   const HeadGroup g = grp ? g1 : g0;
-  const int P0 = (blockIdx.x - grp * per_group) * kPx;
+  const int wg = blockIdx.x - grp * per_group;
   const int hw = s.h * s.w;
   const int total = s.n * hw;
   constexpr int xpitch = CI * 4 + 16;  // +16 B: consecutive pixels start 4 banks apart
@@ -87,6 +94,10 @@ __global__ __launch_bounds__(256, ONE ? 4 / PXB : 2 / PXB) void conv_head_bf16x3
     }
   };
   load_a1(0);
+  for (int tile = 0; tile < TPW; ++tile) {
+  const int P0 = (wg * TPW + tile) * kPx;
+  if (P0 >= total) break;  // block-uniform
+  if (!ONE && tile > 0) load_a1(0);
   // ---- input tile -> LDS (16-B pieces; pixels past the batch repeat the last one) ----
   {
     // (chunk-planar input: consecutive threads take consecutive pixels of one plane, so a wave
@@ -224,14 +235,22 @@ __global__ __launch_bounds__(256, ONE ? 4 / PXB : 2 / PXB) void conv_head_bf16x3
     if (o32) *(floatx4*)(o32 + co) = v;
   }
   }
+  }
 }
 
 template <int NB2, int PXB>
 static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st) {
   constexpr int kPx = kHeadPx * PXB;
   const int total = s.n * s.h * s.w;
-  const int per = (total + kPx - 1) / kPx;
   const bool one = s.co1 == 128;
+  // OP_HEAD_TPW=2 / 4: Mconv6 + Mconv7 with that many tiles per workgroup -- opt-in: 2.28 vs 2.14
+  // ms per 232-frame step at TPW 4 (4-round A/B, profiles/r04/ab_r04t_head_tpw.log), so the heads
+  // are not bound by re-reading their weights from L2 (2 workgroups per CU: 2.82)
+  static const int tpw_env = getenv("OP_HEAD_TPW") ? atoi(getenv("OP_HEAD_TPW")) : 0;
+  const int tiles = (total + kPx - 1) / kPx;
+  int tpw = 1;
+  if (one && PXB == 1 && (tpw_env == 2 || tpw_env == 4)) tpw = tpw_env;
+  const int per = (tiles + tpw - 1) / tpw;
   const int lds = kPx * (128 * 4 + 16) * (one ? 1 : 2);
   static bool attr = false;
   if (!attr) {
@@ -239,9 +258,19 @@ static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, true, PXB>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, true, PXB, 2>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, true, PXB, 4>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  if (one)
+  if (one && tpw == 4)
+    hipLaunchKernelGGL((conv_head_bf16x3<NB2, true, PXB, 4>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s,
+                       g[0], s.groups > 1 ? g[1] : g[0], per);
+  else if (one && tpw == 2)
+    hipLaunchKernelGGL((conv_head_bf16x3<NB2, true, PXB, 2>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s,
+                       g[0], s.groups > 1 ? g[1] : g[0], per);
+  else if (one)
     hipLaunchKernelGGL((conv_head_bf16x3<NB2, true, PXB>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s,
                        g[0], s.groups > 1 ? g[1] : g[0], per);
   else
