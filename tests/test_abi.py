@@ -76,3 +76,18 @@ def test_loader_leaves_the_environment_alone(preset):
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().splitlines()[-1] == "True %s" % preset
+
+
+def test_census_and_profile_slots_mirror_the_header(lib):
+    """_lib.CENSUS / CENSUS_SLOTS / PROFILE_CLASSES name exactly the header's OP_CENSUS_* and
+    OP_PROFILE_CLASSES slots (the census and profile readers index C arrays by them)."""
+    src = open(os.path.join(REPO, "include", "openpose_hip.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+(OP_CENSUS_[A-Z0-9_]+)\s+(\d+)", src)}
+    assert defs.pop("OP_CENSUS_SLOTS") == lib.CENSUS_SLOTS
+    named = {k: v for k, v in defs.items()}
+    assert sorted(lib.CENSUS.values()) == sorted(v for v in named.values() if v >= 11)
+    for name, slot in lib.CENSUS.items():
+        assert named["OP_CENSUS_" + name.upper()] == slot, name
+    assert all(v < lib.CENSUS_SLOTS for v in named.values())
+    m = re.search(r"#define\s+OP_PROFILE_CLASSES\s+(\d+)", src)
+    assert int(m.group(1)) == len(lib.Context.PROFILE_CLASSES)
