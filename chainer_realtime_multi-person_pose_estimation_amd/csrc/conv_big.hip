@@ -927,6 +927,7 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
       static const bool joint = !(getenv("OP_M16_JOINT") && atoi(getenv("OP_M16_JOINT")) == 0);  // A/B aid
       static const double gamma = getenv("OP_M16_SPLIT_GAMMA") ? atof(getenv("OP_M16_SPLIT_GAMMA")) : 0.2;
+      static const bool plain_small = !(getenv("OP_M16_PLAIN_SMALL") && atoi(getenv("OP_M16_PLAIN_SMALL")) == 0);
       auto wgs_of = [](const BigTiling& t) -> int {
         return t.xpu ? 8 * ((t.per_unit + t.xpu - 1) / t.xpu) * (t.pair > 1 ? t.pair : 1) : t.units * t.per_unit;
       };
@@ -977,15 +978,25 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
               BigTiling tc{};
               if (!raster_tiling(k, s.n, s.h, s.w, s.groups, cop_max, tc, true)) continue;
               pairmaj(tc);
-              for (int sp : {2, 3, 4, 6, 8, 12, 16}) {
-                if (s.c16 % sp) continue;
-                const int r = (wgs_of(tc) * sp + 255) / 256;
-                const double cost = (double)r * (s.c16 / sp) * (2 + cand) + gamma * sp;
-                if (cost < best) {
-                  best = cost;
-                  npx = cand;
-                  tl = tc;
-                  S = sp;
+              // round 4: also the plain block order -- the XCD-aware grid pads each XCD's share of
+              // a weight set to whole slots, so a split launch of few tiles (one frame's Mconv1: 9
+              // tiles x 2 sets x 12 splits = 216 workgroups) takes a second round it does not need
+              // (288 grid slots); plain order keeps such a launch in one (OP_M16_PLAIN_SMALL=0: off)
+              BigTiling tp = tc;
+              tp.xpu = 0;
+              tp.pair = 1;
+              for (int ord = 0; ord < (plain_small ? 2 : 1); ++ord) {
+                const BigTiling& tt = ord ? tp : tc;
+                for (int sp : {2, 3, 4, 6, 8, 12, 16}) {
+                  if (s.c16 % sp) continue;
+                  const int r = (wgs_of(tt) * sp + 255) / 256;
+                  const double cost = (double)r * (s.c16 / sp) * (2 + cand) + gamma * sp;
+                  if (cost < best) {
+                    best = cost;
+                    npx = cand;
+                    tl = tt;
+                    S = sp;
+                  }
                 }
               }
             }
