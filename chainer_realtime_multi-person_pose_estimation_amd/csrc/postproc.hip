@@ -511,6 +511,15 @@ __global__ __launch_bounds__(256) void limb_greedy(PostShape s, PostBuffers b) {
   if (tid == 0) b.conn_cnt[fl] = got;
 }
 
+// wave-uniform-lane broadcasts (v_readlane_b32): lane must be the same for every lane of the wave
+__device__ __forceinline__ int rl_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ double rl_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // grouping_key_points + subsets_to_pose_array, one wave per frame.
 // kBig: the subsets live in HBM (b.sub_ids / b.sub_sc, b.maxs rows, int32 peak ids) for any
 // peak and subset count; otherwise in LDS (<= kMaxSubsetsLds rows, int16 ids).
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
     return (double)b.peak_score[((int64_t)f * OP_N_JOINTS + joint) * b.maxp + (id - base[joint])];
   };
   auto fetch = [&](int l, int cb, int& ia, int& ib, double& sc) {
-    const int K = __shfl(kc, l);
+    const int K = rl_i(kc, l);
     ia = 0;
     ib = 0;
     sc = 0.0;
@@ -585,7 +594,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   fetch(0, 0, nx_ia, nx_ib, nx_sc);
   for (int l = 0; l < OP_N_LIMBS && status == OP_OK; ++l) {
     const int ja = s.limbs[l][0], jb = s.limbs[l][1];
-    const int K = __shfl(kc, l);
+    const int K = rl_i(kc, l);
     int my_ia = nx_ia, my_ib = nx_ib;
     double my_sc = nx_sc;
     if (l + 1 < OP_N_LIMBS) fetch(l + 1, 0, nx_ia, nx_ib, nx_sc);
@@ -598,10 +607,12 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
     }
     const int ce = min(K - cb, 64);
     for (int c = 0; c < ce && status == OP_OK; ++c) {
-      const int ia = __shfl(my_ia, c);
-      const int ib = __shfl(my_ib, c);
-      const double score = __shfl(my_sc, c);
-      const double psa = __shfl(my_pa, c), psb = __shfl(my_pb, c);  // pscore(ja, ia), pscore(jb, ib)
+      // lane c's values, read with v_readlane into scalar registers (c is wave-uniform): no LDS
+      // round trip per broadcast, as __shfl's ds_bpermute would make (8 per connection)
+      const int ia = rl_i(my_ia, c);
+      const int ib = rl_i(my_ib, c);
+      const double score = rl_d(my_sc, c);
+      const double psa = rl_d(my_pa, c), psb = rl_d(my_pb, c);  // pscore(ja, ia), pscore(jb, ib)
       int found = 0, f0 = -1, f1 = -1;
       for (int s0 = 0; s0 < S; s0 += 64) {
         const int r = s0 + lane;
