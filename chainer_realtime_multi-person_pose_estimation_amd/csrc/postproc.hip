@@ -1038,10 +1038,23 @@ __global__ __launch_bounds__(256) void peak_sort_rank(const int32_t* __restrict_
   }
 }
 
+// The step's counters zeroed by one launch (round 4): a hipMemsetAsync of a few dozen bytes runs as
+// two fill kernels on this stack, four per frame for the peak and candidate counters
+__global__ __launch_bounds__(256) void zero_counters(int32_t* __restrict__ a, int na, int32_t* __restrict__ b, int nb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < na) a[i] = 0;
+  else if (i - na < nb && b) b[i - na] = 0;
+}
+
+// also / also_n: a second counter array zeroed by the same launch (the candidate counts of the
+// connection step that follows), or null
 template <class Src>
-static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st) {
+static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hipStream_t st, int32_t* also = nullptr,
+                          int also_n = 0) {
   const int planes = s.n * OP_N_JOINTS;
-  OP_HIP_CHECK(hipMemsetAsync(b.peak_cnt, 0, sizeof(int32_t) * planes, st));
+  hipLaunchKernelGGL(zero_counters, dim3((unsigned)((planes + also_n + 255) / 256)), dim3(256), 0, st, b.peak_cnt, planes,
+                     also, also ? also_n : 0);
+  OP_AFTER_LAUNCH("zero_counters", st);
   const int tx = (s.mw + kFT - 1) / kFT, ty = (s.mh + kFT - 1) / kFT;
   const dim3 g((unsigned)(8 * ((s.n + 7) / 8) * tx * ty * OP_N_JOINTS));
   if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
@@ -1110,8 +1123,7 @@ int launch_post_maps(const MapSource& src, const PostShape& s, PostBuffers& b, h
   hs.lw = s.lw;
   hs.mh = s.mh;
   hs.mw = s.mw;
-  if ((rc = run_heat_tiled(hs, s, b, st))) return rc;
-  OP_HIP_CHECK(hipMemsetAsync(b.cand_cnt, 0, sizeof(int32_t) * s.n * OP_N_LIMBS, st));
+  if ((rc = run_heat_tiled(hs, s, b, st, b.cand_cnt, s.n * OP_N_LIMBS))) return rc;  // zeroes cand_cnt too
   // axis-tap tables in LDS when they fit 48 KiB (368 x 368 maps: 17 KiB; 1280 x 720: 47 KiB), and
   // the limb's two low-res PAF planes next to them when both fit 64 KiB (46 x 46: +17 KiB): the
   // 80 map reads per candidate pair hit LDS instead of scattered L2 lines
