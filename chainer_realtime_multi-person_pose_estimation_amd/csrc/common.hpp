@@ -206,8 +206,10 @@ int launch_conv1_pair(const uint8_t* frames, int64_t frame_bytes, int64_t row_st
                       const void* w12, const float* b12, float* out, int32_t pout, hipStream_t st);
 
 // ---- multi-scale path (precise.hip) ----
+// n frames: frame f at bgr + f * src_fstride bytes -> out + f * dst_ffloats floats (one launch)
 int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
-                            int32_t ph, int32_t pw, bool split, float* out, hipStream_t st);
+                            int32_t ph, int32_t pw, bool split, float* out, int32_t n, int64_t src_fstride,
+                            int64_t dst_ffloats, hipStream_t st);
 int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, int32_t sh, int32_t sw, int32_t cn,
                             float* dst, int32_t dh, int32_t dw, int32_t mode, float div, hipStream_t st);
 // mode 1 (planar destination) for n frames at once (source / destination frame strides in floats):
@@ -222,12 +224,18 @@ int launch_resize_cubic_f32_frames(const float* src, int64_t sstride, int32_t ps
 struct CubicMeanArgs {
   const float* src[OP_MAX_SCALES];
   int64_t cstride[OP_MAX_SCALES], sstride[OP_MAX_SCALES];
+  int64_t fstride[OP_MAX_SCALES];  // floats per frame (the _rows form: every frame in one launch)
   int sh[OP_MAX_SCALES], sw[OP_MAX_SCALES];
   double scx[OP_MAX_SCALES], scy[OP_MAX_SCALES];
   int ns;
 };
 int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int32_t dh, int32_t dw, int32_t npaf,
                                         int32_t nheat, hipStream_t st);
+// n frames (src[k] = frame 0, fstride[k] apart; dst frames dst_fstride apart); *taken false when
+// a scale's rows would exceed its LDS budget (then run the per-frame form)
+int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
+                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
+                                             bool* taken);
 // detect_precise's two map resizes per scale fused (round 4): the padded-size maps are never
 // written; see precise.hip resize_cubic_fused_mean.  low[k]: scale k's last-stage maps, planar
 // [frame][npaf + nheat][lh][lw] f32 (launch_maps_planar).

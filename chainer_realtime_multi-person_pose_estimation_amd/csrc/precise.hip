@@ -13,12 +13,16 @@ __device__ __forceinline__ float norm_u8(int v) { return __fsub_rn(__fdiv_rn((fl
 // resize of the frame, the rest the pad colour (104, 117, 123) (pose_detector.py:446, :46-55),
 // normalised (x/255 - 0.5, :426-431).  SPLIT: 16 channels as bf16 hi/lo (split format), else
 // 8 f32 channels.
+// Frame blockIdx.y of the batch: bgr + y * src_fstride bytes -> out + y * dst_fbytes.
 template <bool SPLIT>
 __global__ __launch_bounds__(256) void preprocess_cubic(const uint8_t* __restrict__ bgr, int64_t row_stride, int sh,
-                                                        int sw, int rh, int rw, int ph, int pw, char* __restrict__ out) {
+                                                        int sw, int rh, int rw, int ph, int pw, char* __restrict__ out,
+                                                        int64_t src_fstride, int64_t dst_fbytes) {
   const int wp = pw + 2, hp = ph + 2;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)hp * wp) return;
+  bgr += blockIdx.y * src_fstride;
+  out += blockIdx.y * dst_fbytes;
   const int px = (int)(i % wp), py = (int)(i / wp);
   float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int dx = px - 1, dy = py - 1;
@@ -57,15 +61,17 @@ __global__ __launch_bounds__(256) void preprocess_cubic(const uint8_t* __restric
 }
 
 int launch_preprocess_cubic(const uint8_t* bgr, int64_t row_stride, int32_t sh, int32_t sw, int32_t rh, int32_t rw,
-                            int32_t ph, int32_t pw, bool split, float* out, hipStream_t st) {
+                            int32_t ph, int32_t pw, bool split, float* out, int32_t n, int64_t src_fstride,
+                            int64_t dst_ffloats, hipStream_t st) {
   const int64_t total = (int64_t)(ph + 2) * (pw + 2);
-  const dim3 grid((unsigned)((total + 255) / 256));
+  const dim3 grid((unsigned)((total + 255) / 256), (unsigned)n);
+  const int64_t dst_fbytes = dst_ffloats * (int64_t)sizeof(float);
   if (split)
     hipLaunchKernelGGL(preprocess_cubic<true>, grid, dim3(256), 0, st, bgr, row_stride, sh, sw, rh, rw, ph, pw,
-                       (char*)out);
+                       (char*)out, src_fstride, dst_fbytes);
   else
     hipLaunchKernelGGL(preprocess_cubic<false>, grid, dim3(256), 0, st, bgr, row_stride, sh, sw, rh, rw, ph, pw,
-                       (char*)out);
+                       (char*)out, src_fstride, dst_fbytes);
   OP_AFTER_LAUNCH("preprocess_cubic", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
@@ -307,6 +313,136 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
                      dim3(256), 0, st, a, dst, dh, dw, npaf, nheat);
   OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean", st);
   OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
+// The same second pass with a block of TY output rows x 256 columns x G channels, every frame in
+// one launch (round 4): per scale a thread makes the horizontal sums of the source rows its block's
+// output rows read ONCE, into its own LDS column (resize_cubic_f32_up's scheme, so no barrier), and
+// every output row's vertical sum from them -- resize_cubic_f32_planar_mean makes four horizontal
+// sums (16 gathers) per output row and scale.  The row taps are made once per scale, the column
+// taps once per (scale, thread).  Each output's f32 operations and their order are unchanged:
+// horizontal sums left to right, the SIMD-body / scalar-tail vertical orders, scales summed in
+// order, one division by the scale count.  LDS: rcap rows x 256 floats (rcap >= the rows any
+// block reads at any scale; the host checks).
+#ifndef ROWS_UNROLL
+#define ROWS_UNROLL 2
+#endif
+template <int G, int TY>
+__global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean_rows(CubicMeanArgs a, float* __restrict__ dst,
+                                                                         int64_t dst_fstride, int dh, int dw, int npaf,
+                                                                         int nheat, int ngroups, int rcap) {
+  extern __shared__ float hsl[];  // [rcap][256], each thread its own column
+  const int tid = threadIdx.x, x = blockIdx.x * 256 + tid;
+  const int y0 = blockIdx.y * TY;
+  const int f = blockIdx.z / ngroups, c0 = (blockIdx.z - f * ngroups) * G;
+  if (x >= dw) return;
+  const int nch = npaf + nheat;
+  const int ylast = min(y0 + TY - 1, dh - 1);
+  float sum[G][TY];
+  for (int k = 0; k < a.ns; ++k) {
+    const int sh = a.sh[k], sw = a.sw[k];
+    const int r0 = cv_cubic_tap_s(y0, a.scy[k]).s - 1;
+    const int nr = cv_cubic_tap_s(ylast, a.scy[k]).s + 2 - r0 + 1;
+    const bool fits = nr <= rcap;  // never false (host bound); else the outputs are NaN
+    CubicTap ty[TY];  // block-uniform: moved to scalar registers
+#pragma unroll
+    for (int yy = 0; yy < TY; ++yy) {
+      const CubicTap t = cv_cubic_tap_s(min(y0 + yy, ylast), a.scy[k]);
+      ty[yy].s = __builtin_amdgcn_readfirstlane(t.s);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ty[yy].c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t.c[j])));
+    }
+    const CubicTap tx = cv_cubic_tap_s(x, a.scx[k]);
+    int col[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j] = clampc(tx.s - 1 + j, 0, sw - 1);
+    const float* pf = a.src[k] + (int64_t)f * a.fstride[k];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {  // unrolled: sum[g] stays in registers
+      const int c = c0 + g;
+      if (c >= nch) break;
+      const bool paf = c < npaf;
+      const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+      const float* p = pf + (int64_t)c * a.cstride[k];
+#pragma unroll ROWS_UNROLL
+      for (int r = 0; r < (fits ? nr : 0); ++r) {  // cv_cubic_f32 (pstride 1): left-to-right horizontal sums
+        const float* row = p + clampc(r0 + r, 0, sh - 1) * (int)a.sstride[k];
+        float h = __fmul_rn(row[col[0]], tx.c[0]);
+        h = __fadd_rn(h, __fmul_rn(row[col[1]], tx.c[1]));
+        h = __fadd_rn(h, __fmul_rn(row[col[2]], tx.c[2]));
+        h = __fadd_rn(h, __fmul_rn(row[col[3]], tx.c[3]));
+        hsl[r * 256 + tid] = h;
+      }
+      const bool simd = x * cn + ce < dw * cn / 4 * 4;
+#pragma unroll
+      for (int yy = 0; yy < TY; ++yy) {
+        const int b = ty[yy].s - 1 - r0;
+        const float h0 = hsl[b * 256 + tid], h1 = hsl[(b + 1) * 256 + tid];
+        const float h2 = hsl[(b + 2) * 256 + tid], h3 = hsl[(b + 3) * 256 + tid];
+        float v;
+        if (!fits) {
+          v = __builtin_nanf("");
+        } else if (simd) {
+          const float t3 = __fmul_rn(h3, ty[yy].c[3]);
+          const float t2 = __fadd_rn(__fmul_rn(h2, ty[yy].c[2]), t3);
+          const float t1 = __fadd_rn(__fmul_rn(h1, ty[yy].c[1]), t2);
+          v = __fadd_rn(__fmul_rn(h0, ty[yy].c[0]), t1);
+        } else {
+          v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty[yy].c[0]), __fmul_rn(h1, ty[yy].c[1])),
+                                  __fmul_rn(h2, ty[yy].c[2])),
+                        __fmul_rn(h3, ty[yy].c[3]));
+        }
+        sum[g][yy] = k == 0 ? v : __fadd_rn(sum[g][yy], v);
+      }
+    }
+  }
+  const int64_t plane = (int64_t)dh * dw;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (c0 + g >= nch) break;
+    float* o = dst + (int64_t)f * dst_fstride + (c0 + g) * plane + (int64_t)y0 * dw + x;
+#pragma unroll
+    for (int yy = 0; yy < TY; ++yy)
+      if (y0 + yy < dh) o[(int64_t)yy * dw] = __fdiv_rn(sum[g][yy], (float)a.ns);
+  }
+}
+
+#ifndef MEAN_ROWS_G
+#define MEAN_ROWS_G 1
+#endif
+#ifndef MEAN_ROWS_TY
+#define MEAN_ROWS_TY 8
+#endif
+int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
+                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
+                                             bool* taken) {
+  constexpr int G = MEAN_ROWS_G, TY = MEAN_ROWS_TY;
+  *taken = false;
+  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
+    set_error("resize_cubic_f32_planar_mean_rows: 1..OP_MAX_SCALES scales");
+    return OP_ERR_INVALID;
+  }
+  // rows TY consecutive outputs read: floor((TY - 1) * s) + 1 distinct tap origins + 3, + 1 for
+  // the f32 rounding of the source coordinate, + 1 spare (as fused_lds)
+  int rcap = 0;
+  for (int k = 0; k < a.ns; ++k) rcap = std::max(rcap, (int)std::floor((TY - 1) * a.scy[k]) + 7);
+  const size_t lds = (size_t)rcap * 256 * sizeof(float);
+  if (lds > 64 * 1024) return OP_OK;  // caller runs resize_cubic_f32_planar_mean
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)resize_cubic_f32_planar_mean_rows<G, TY>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr = true;
+  }
+  const int ngroups = (npaf + nheat + G - 1) / G;
+  hipLaunchKernelGGL((resize_cubic_f32_planar_mean_rows<G, TY>),
+                     dim3((unsigned)((dw + 255) / 256), (unsigned)((dh + TY - 1) / TY), (unsigned)(n * ngroups)),
+                     dim3(256), lds, st, a, dst, dst_fstride, dh, dw, npaf, nheat, ngroups, rcap);
+  OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean_rows", st);
+  OP_HIP_CHECK(hipGetLastError());
+  *taken = true;
   return OP_OK;
 }
 

@@ -2735,10 +2735,8 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
     RC(ensure_geometry(c, n, ph, pw));
     const Act& x0 = c->buf[B_X0];
     RC(profiled(c, kProfInput, 0.0, 0.0, [&] {
-      for (int f = 0; f < n; ++f)
-        RC(launch_preprocess_cubic(c->d_frames + f * fbytes, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split,
-                                   x0.p + (size_t)f * x0.frame_floats(), c->stream));
-      return OP_OK;
+      return launch_preprocess_cubic(c->d_frames, (int64_t)w * 3, h, w, rh, rw, ph, pw, c->split, x0.p, n,
+                                     (int64_t)fbytes, (int64_t)x0.frame_floats(), c->stream);
     }));
     RC(run_forward(c));
     // last-stage maps (lh, lw, cs) with the PAF / heat channels at paf_off / heat_off
@@ -2801,7 +2799,32 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       return OP_ERR_STATE;
     }
   }
-  for (int f = 0; f < n && !fused; ++f) {
+  // round 4: every frame in one launch, a block of 8 output rows making each source row's
+  // horizontal sums once (resize_cubic_f32_planar_mean_rows); OP_CUBIC_ROWS=0 selects the per-frame
+  // form (A/B aid, read per call)
+  bool rows_done = false;
+  const char* renv = getenv("OP_CUBIC_ROWS");
+  if (!fused && !(renv && atoi(renv) == 0)) {
+    CubicMeanArgs a{};
+    a.ns = ns;
+    for (int k = 0; k < ns; ++k) {
+      const int64_t pp = (int64_t)phs[k] * pws[k];
+      a.src[k] = c->d_pmid + mid_off[k];
+      a.fstride[k] = pp * (OP_N_PAF + OP_N_HEAT);
+      a.cstride[k] = pp;
+      a.sstride[k] = pws[k];
+      a.sh[k] = rhs[k];
+      a.sw[k] = rws[k];
+      a.scx[k] = 1.0 / ((double)w / (double)rws[k]);  // cv_cubic_scale (cvcubic.hpp)
+      a.scy[k] = 1.0 / ((double)h / (double)rhs[k]);
+    }
+    RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+      return launch_resize_cubic_f32_planar_mean_rows(a, c->d_psum, fplanes, n, h, w, OP_N_PAF, OP_N_HEAT, c->stream,
+                                                      &rows_done);
+    }));
+  }
+  if (rows_done) census_add(OP_CENSUS_CUBIC_ROWS);
+  for (int f = 0; f < n && !fused && !rows_done; ++f) {
     CubicMeanArgs a{};
     a.ns = ns;
     for (int k = 0; k < ns; ++k) {

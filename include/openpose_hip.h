@@ -298,6 +298,8 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_CUBIC_FUSED 25 /* detect_precise map resizes as one fused pass (resize_cubic_fused_mean) */
 #define OP_CENSUS_CUBIC_TWO_PASS 26 /* ... as the two-pass path (padded-size maps in HBM) */
 #define OP_CENSUS_SPLITK_INKERNEL 27 /* split-K launches (7x7 or 3x3) finished by their last split, no reduce launch */
+#define OP_CENSUS_CUBIC_ROWS 28  /* two-pass second resize as one row-block launch for the batch
+                                    (resize_cubic_f32_planar_mean_rows), else one launch per frame */
 #define OP_CENSUS_SLOTS 32
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

@@ -171,3 +171,43 @@ def test_fused_map_resize_equals_two_pass(lib, rand_weights, shape, n, monkeypat
         assert np.array_equal(p1, p0) and np.array_equal(h1, h0)
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("shape,n", [((H, W), 3), ((481, 643), 2), ((96, 128), 2)])
+def test_row_block_map_resize_equals_per_frame(lib, rand_weights, shape, n, monkeypatch):
+    """Round 4: the two-pass path's second resize (every scale's crop cubic-resized to the frame
+    size, summed in scale order, divided by the scale count) as one launch for the batch with blocks
+    of 8 output rows that make each source row's horizontal sums once
+    (precise.hip resize_cubic_f32_planar_mean_rows, the default) is BIT-IDENTICAL to the per-frame
+    form (OP_CUBIC_ROWS=0, resize_cubic_f32_planar_mean, held to the oracle above); the census shows
+    which ran."""
+    Wt = _weights(rand_weights)
+    limits = lib.OpLimits()
+    limits.max_peaks_per_joint = 2048
+    c = lib.Context(0, None, limits)
+    h, w = shape
+    try:
+        c.set_weights(Wt)
+        c.set_batch_invariant(True)
+        frames = np.stack([_crowd_frame(21 + i)[:h, :w] for i in range(n)])
+        out = {}
+        for rows in ("1", "0"):
+            monkeypatch.setenv("OP_CUBIC_ROWS", rows)
+            c.stage_frames(frames)
+            lib.conv_census(reset=True)
+            try:
+                c.run_staged_precise()
+            except IndexError:
+                pass
+            c.synchronize()
+            cen = lib.conv_census(reset=True)
+            out[rows] = (c.fetch_maps(0, n), cen)
+        (p1, h1), cen1 = out["1"]
+        (p0, h0), cen0 = out["0"]
+        assert cen1["cubic_two_pass"] == 1 and cen1["cubic_rows"] == 1
+        assert cen0["cubic_two_pass"] == 1 and cen0["cubic_rows"] == 0
+        assert p1.shape == (n, 38, h, w) and h1.shape == (n, 19, h, w)
+        assert np.isfinite(p1).all() and np.isfinite(h1).all()
+        assert np.array_equal(p1, p0) and np.array_equal(h1, h0)
+    finally:
+        c.close()

@@ -1,6 +1,7 @@
 """Interleaved A/B of library builds (OP_LIB_VARIANT) or environment settings with per-class times:
 each variant runs in its own child process per round (a process loads one library).
-usage: ab_lib.py ROUNDS base v1 NAME=VALUE[,NAME=VALUE] ...  (an '=' spec sets env vars, product lib)"""
+usage: ab_lib.py ROUNDS base v1 NAME=VALUE[,NAME=VALUE] ...  (an '=' spec sets env vars, product lib)
+AB_BENCH_ARGS: extra bench.py arguments (e.g. "--precise --frame 720x1280 --steps 5")."""
 import json
 import os
 import subprocess
@@ -17,7 +18,8 @@ for r in range(rounds):
         else:
             env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
         p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--no-variants", "--steps", "10",
-                            "--warmup", "2"], env=env, capture_output=True, text=True, timeout=300)
+                            "--warmup", "2"] + os.environ.get("AB_BENCH_ARGS", "").split(), env=env, capture_output=True,
+                           text=True, timeout=300)
         if p.returncode:
             print(p.stdout[-2000:], p.stderr[-2000:])
             sys.exit(p.returncode)
@@ -28,5 +30,6 @@ for v in variants:
     vals = sorted(x[0] for x in out[v])
     c3 = sorted(x[1]["conv3x3"] for x in out[v])
     c7 = sorted(x[1]["conv7x7"] for x in out[v])
-    print("%-8s fps median %.1f | conv3x3 median %.3f | conv7x7 median %.3f" % (v, vals[len(vals) // 2], c3[len(c3) // 2],
-                                                                           c7[len(c7) // 2]))
+    mr = sorted(x[1].get("map_resize", 0.0) for x in out[v])
+    print("%-8s fps median %.1f | conv3x3 median %.3f | conv7x7 median %.3f | map_resize median %.3f" %
+          (v, vals[len(vals) // 2], c3[len(c3) // 2], c7[len(c7) // 2], mr[len(mr) // 2]))
