@@ -236,6 +236,9 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
 int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
                                              int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
                                              bool* taken);
+int launch_resize_cubic_f32_planar_mean_tile(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
+                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
+                                             bool* taken);
 // detect_precise's two map resizes per scale fused (round 4): the padded-size maps are never
 // written; see precise.hip resize_cubic_fused_mean.  low[k]: scale k's last-stage maps, planar
 // [frame][npaf + nheat][lh][lw] f32 (launch_maps_planar).

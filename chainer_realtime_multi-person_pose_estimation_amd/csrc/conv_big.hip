@@ -944,10 +944,14 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
           tl = std::get<1>(it->second);
           S = std::get<2>(it->second);
         } else {
+          // round 4: NPX 9 and 7 as well (OP_M16_ODD=0: off), e.g. the C4 scale-1.5 launches: 472
+          // workgroups of 576 px in 2 rounds instead of 448 of 640 px (1.75 rounds, cost 22 vs 24)
+          static const bool odd = !(getenv("OP_M16_ODD") && atoi(getenv("OP_M16_ODD")) == 0);
           if (force != 10) {
             int best = rounds(tl) * (2 + 10);
-            for (int cand : {8, 6, 5, 4, 3, 2}) {
+            for (int cand : {9, 8, 7, 6, 5, 4, 3, 2}) {
               if (force && cand != force) continue;
+              if (!odd && (cand == 9 || cand == 7)) continue;
               BigConfig k{7, 1, 8, 128, 1, 1};
               k.cap_px = 64 * cand;
               BigTiling tc{};
@@ -971,8 +975,10 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
               }
           } else if (s.splitk && wgs_of(tl) < 256) {
             double best = (double)rounds(tl) * s.c16 * (2 + npx);
-            for (int cand : {10, 8, 6, 5, 4, 3, 2}) {
+            static const bool odd_split = getenv("OP_M16_ODD_SPLIT") && atoi(getenv("OP_M16_ODD_SPLIT")) == 1;
+            for (int cand : {10, 9, 8, 7, 6, 5, 4, 3, 2}) {
               if (force && cand != force) continue;
+              if (!odd_split && (cand == 9 || cand == 7)) continue;
               BigConfig k{7, 1, 8, 128, 1, 1};
               k.cap_px = 64 * cand;
               BigTiling tc{};

@@ -288,7 +288,8 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                    const SplitConvGroup& g1, const BigTiling& tl) {
   static bool attr = false;
   if (!attr) {
-    const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 8>,
+    const void* fns[] = {(const void*)conv_m16_bf16x3<7, 10>, (const void*)conv_m16_bf16x3<7, 9>,
+                         (const void*)conv_m16_bf16x3<7, 8>,  (const void*)conv_m16_bf16x3<7, 7>,
                          (const void*)conv_m16_bf16x3<7, 6>,
                          (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
                          (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>,
@@ -311,7 +312,9 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
   switch (npx) {
+    case 9: hipLaunchKernelGGL((conv_m16_bf16x3<7, 9>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
     case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
+    case 7: hipLaunchKernelGGL((conv_m16_bf16x3<7, 7>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
     case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
     case 5:
       if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 5, true>), grid, dim3(512), lds, st, s, g0, g1, tl);

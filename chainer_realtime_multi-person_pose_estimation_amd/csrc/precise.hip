@@ -328,8 +328,11 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
 #ifndef ROWS_UNROLL
 #define ROWS_UNROLL 2
 #endif
+#ifndef ROWS_MINB
+#define ROWS_MINB 1
+#endif
 template <int G, int TY>
-__global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean_rows(CubicMeanArgs a, float* __restrict__ dst,
+__global__ __launch_bounds__(256, ROWS_MINB) void resize_cubic_f32_planar_mean_rows(CubicMeanArgs a, float* __restrict__ dst,
                                                                          int64_t dst_fstride, int dh, int dw, int npaf,
                                                                          int nheat, int ngroups, int rcap) {
   extern __shared__ float hsl[];  // [rcap][256], each thread its own column
@@ -441,6 +444,147 @@ int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst,
                      dim3((unsigned)((dw + 255) / 256), (unsigned)((dh + TY - 1) / TY), (unsigned)(n * ngroups)),
                      dim3(256), lds, st, a, dst, dst_fstride, dh, dw, npaf, nheat, ngroups, rcap);
   OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean_rows", st);
+  OP_HIP_CHECK(hipGetLastError());
+  *taken = true;
+  return OP_OK;
+}
+
+// The row-block second pass with each scale's source tile staged in LDS: the block's nr source
+// rows x the ~256 * s + 4 source columns its outputs read are loaded once, coalesced (a row
+// segment per pass of the block), and the four column taps of every horizontal sum come from LDS
+// instead of four gathers from global memory per row.  One channel per block; the horizontal sums
+// go to the thread's own LDS column as in _rows; the f32 operations and their order are unchanged.
+// LDS: T [rcap][ccap] source tile + H [rcap][256] horizontal sums; rcap <= kTileRows, ccap <= 512.
+constexpr int kTileRows = 16;
+template <int TY>
+__global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean_tile(CubicMeanArgs a, float* __restrict__ dst,
+                                                                         int64_t dst_fstride, int dh, int dw, int npaf,
+                                                                         int nheat, int rcap, int ccap) {
+  extern __shared__ float lds_t[];
+  float* T = lds_t;                 // [rcap][ccap]
+  float* H = lds_t + rcap * ccap;   // [rcap][256]
+  const int nch = npaf + nheat;
+  const int tid = threadIdx.x, x0 = blockIdx.x * 256, x = x0 + tid;
+  const int y0 = blockIdx.y * TY;
+  const int f = blockIdx.z / nch, c = blockIdx.z - f * nch;
+  const bool live = x < dw;
+  const int xc = min(x, dw - 1), xl = min(x0 + 255, dw - 1);
+  const int ylast = min(y0 + TY - 1, dh - 1);
+  const bool paf = c < npaf;
+  const int cn = paf ? npaf : nheat, ce = paf ? c : c - npaf;
+  const bool simd = xc * cn + ce < dw * cn / 4 * 4;
+  float sum[TY];
+  for (int k = 0; k < a.ns; ++k) {
+    const int sh = a.sh[k], sw = a.sw[k];
+    const int r0 = cv_cubic_tap_s(y0, a.scy[k]).s - 1;
+    const int nr = cv_cubic_tap_s(ylast, a.scy[k]).s + 2 - r0 + 1;
+    const int cx0 = clampc(cv_cubic_tap_s(x0, a.scx[k]).s - 1, 0, sw - 1);
+    const int nc = clampc(cv_cubic_tap_s(xl, a.scx[k]).s + 2, 0, sw - 1) - cx0 + 1;
+    const bool fits = nr <= rcap && nc <= ccap;  // never false (host bounds); else the outputs are NaN
+    CubicTap ty[TY];  // block-uniform: scalar registers
+#pragma unroll
+    for (int yy = 0; yy < TY; ++yy) {
+      const CubicTap t = cv_cubic_tap_s(min(y0 + yy, ylast), a.scy[k]);
+      ty[yy].s = __builtin_amdgcn_readfirstlane(t.s);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ty[yy].c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t.c[j])));
+    }
+    const CubicTap tx = cv_cubic_tap_s(xc, a.scx[k]);
+    int col[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j] = clampc(tx.s - 1 + j, 0, sw - 1) - cx0;
+    const float* p = a.src[k] + (int64_t)f * a.fstride[k] + (int64_t)c * a.cstride[k] + cx0;
+    if (k) __syncthreads();  // the previous scale's horizontal sums have read T
+    if (fits) {  // every row's loads issued before the first LDS store (one memory latency per scale)
+      float v0[kTileRows], v1[kTileRows];
+      const bool c0ok = tid < nc, c1ok = tid + 256 < nc;
+#pragma unroll
+      for (int r = 0; r < kTileRows; ++r) {
+        const float* row = p + clampc(r0 + min(r, nr - 1), 0, sh - 1) * (int)a.sstride[k];
+        v0[r] = c0ok ? row[tid] : 0.f;
+        v1[r] = c1ok ? row[tid + 256] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < kTileRows; ++r) {
+        if (r < nr) {
+          if (c0ok) T[r * ccap + tid] = v0[r];
+          if (c1ok) T[r * ccap + tid + 256] = v1[r];
+        }
+      }
+    }
+    __syncthreads();
+    if (fits) {
+#pragma unroll 2
+      for (int r = 0; r < nr; ++r) {  // cv_cubic_f32 (pstride 1): left-to-right horizontal sums
+        const float* row = T + r * ccap;
+        float h = __fmul_rn(row[col[0]], tx.c[0]);
+        h = __fadd_rn(h, __fmul_rn(row[col[1]], tx.c[1]));
+        h = __fadd_rn(h, __fmul_rn(row[col[2]], tx.c[2]));
+        h = __fadd_rn(h, __fmul_rn(row[col[3]], tx.c[3]));
+        H[r * 256 + tid] = h;
+      }
+    }
+#pragma unroll
+    for (int yy = 0; yy < TY; ++yy) {
+      const int b = ty[yy].s - 1 - r0;
+      float v;
+      if (!fits) {
+        v = __builtin_nanf("");
+      } else {
+        const float h0 = H[b * 256 + tid], h1 = H[(b + 1) * 256 + tid];
+        const float h2 = H[(b + 2) * 256 + tid], h3 = H[(b + 3) * 256 + tid];
+        if (simd) {
+          const float t3 = __fmul_rn(h3, ty[yy].c[3]);
+          const float t2 = __fadd_rn(__fmul_rn(h2, ty[yy].c[2]), t3);
+          const float t1 = __fadd_rn(__fmul_rn(h1, ty[yy].c[1]), t2);
+          v = __fadd_rn(__fmul_rn(h0, ty[yy].c[0]), t1);
+        } else {
+          v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty[yy].c[0]), __fmul_rn(h1, ty[yy].c[1])),
+                                  __fmul_rn(h2, ty[yy].c[2])),
+                        __fmul_rn(h3, ty[yy].c[3]));
+        }
+      }
+      sum[yy] = k == 0 ? v : __fadd_rn(sum[yy], v);
+    }
+  }
+  if (live) {
+    float* o = dst + (int64_t)f * dst_fstride + (int64_t)c * dh * dw + (int64_t)y0 * dw + x;
+#pragma unroll
+    for (int yy = 0; yy < TY; ++yy)
+      if (y0 + yy < dh) o[(int64_t)yy * dw] = __fdiv_rn(sum[yy], (float)a.ns);
+  }
+}
+
+int launch_resize_cubic_f32_planar_mean_tile(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
+                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
+                                             bool* taken) {
+  constexpr int TY = 8;
+  *taken = false;
+  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
+    set_error("resize_cubic_f32_planar_mean_tile: 1..OP_MAX_SCALES scales");
+    return OP_ERR_INVALID;
+  }
+  // extents as in _rows: T consecutive outputs read floor((T - 1) * s) + 5 source indices, + 1
+  // for the f32 rounding of the coordinate, + 1 spare; columns padded to an odd count (banks)
+  int rcap = 0, ccap = 0;
+  for (int k = 0; k < a.ns; ++k) {
+    rcap = std::max(rcap, (int)std::floor((TY - 1) * a.scy[k]) + 7);
+    ccap = std::max(ccap, std::min((int)std::floor(255 * a.scx[k]) + 7, a.sw[k]));
+  }
+  ccap |= 1;
+  const size_t lds = (size_t)rcap * (ccap + 256) * sizeof(float);
+  if (lds > 64 * 1024 || rcap > kTileRows || ccap > 512) return OP_OK;  // caller runs another form
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)resize_cubic_f32_planar_mean_tile<TY>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((resize_cubic_f32_planar_mean_tile<TY>),
+                     dim3((unsigned)((dw + 255) / 256), (unsigned)((dh + TY - 1) / TY), (unsigned)(n * (npaf + nheat))),
+                     dim3(256), lds, st, a, dst, dst_fstride, dh, dw, npaf, nheat, rcap, ccap);
+  OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean_tile", st);
   OP_HIP_CHECK(hipGetLastError());
   *taken = true;
   return OP_OK;

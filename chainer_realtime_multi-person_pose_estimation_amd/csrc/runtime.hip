@@ -2818,7 +2818,13 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
       a.scx[k] = 1.0 / ((double)w / (double)rws[k]);  // cv_cubic_scale (cvcubic.hpp)
       a.scy[k] = 1.0 / ((double)h / (double)rhs[k]);
     }
+    const char* tenv = getenv("OP_CUBIC_TILE");
+    const bool tile = tenv && atoi(tenv) == 1;
     RC(profiled(c, kProfMapResize, 0.0, 0.0, [&] {
+      if (tile)
+        RC(launch_resize_cubic_f32_planar_mean_tile(a, c->d_psum, fplanes, n, h, w, OP_N_PAF, OP_N_HEAT, c->stream,
+                                                    &rows_done));
+      if (rows_done) return OP_OK;
       return launch_resize_cubic_f32_planar_mean_rows(a, c->d_psum, fplanes, n, h, w, OP_N_PAF, OP_N_HEAT, c->stream,
                                                       &rows_done);
     }));

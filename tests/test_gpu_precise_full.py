@@ -178,8 +178,9 @@ def test_row_block_map_resize_equals_per_frame(lib, rand_weights, shape, n, monk
     """Round 4: the two-pass path's second resize (every scale's crop cubic-resized to the frame
     size, summed in scale order, divided by the scale count) as one launch for the batch with blocks
     of 8 output rows that make each source row's horizontal sums once
-    (precise.hip resize_cubic_f32_planar_mean_rows, the default) is BIT-IDENTICAL to the per-frame
-    form (OP_CUBIC_ROWS=0, resize_cubic_f32_planar_mean, held to the oracle above); the census shows
+    (precise.hip resize_cubic_f32_planar_mean_rows, the default) and its form with each scale's
+    source tile staged in LDS (_tile, OP_CUBIC_TILE=1) are BIT-IDENTICAL to the per-frame form
+    (OP_CUBIC_ROWS=0, resize_cubic_f32_planar_mean, held to the oracle above); the census shows
     which ran."""
     Wt = _weights(rand_weights)
     limits = lib.OpLimits()
@@ -191,8 +192,9 @@ def test_row_block_map_resize_equals_per_frame(lib, rand_weights, shape, n, monk
         c.set_batch_invariant(True)
         frames = np.stack([_crowd_frame(21 + i)[:h, :w] for i in range(n)])
         out = {}
-        for rows in ("1", "0"):
-            monkeypatch.setenv("OP_CUBIC_ROWS", rows)
+        for rows in ("tile", "1", "0"):  # tile: the LDS-staged form (OP_CUBIC_TILE=1)
+            monkeypatch.setenv("OP_CUBIC_ROWS", "0" if rows == "0" else "1")
+            monkeypatch.setenv("OP_CUBIC_TILE", "1" if rows == "tile" else "0")
             c.stage_frames(frames)
             lib.conv_census(reset=True)
             try:
@@ -204,6 +206,9 @@ def test_row_block_map_resize_equals_per_frame(lib, rand_weights, shape, n, monk
             out[rows] = (c.fetch_maps(0, n), cen)
         (p1, h1), cen1 = out["1"]
         (p0, h0), cen0 = out["0"]
+        (pt, ht), cent = out["tile"]
+        assert cent["cubic_two_pass"] == 1 and cent["cubic_rows"] == 1
+        assert np.array_equal(pt, p0) and np.array_equal(ht, h0)
         assert cen1["cubic_two_pass"] == 1 and cen1["cubic_rows"] == 1
         assert cen0["cubic_two_pass"] == 1 and cen0["cubic_rows"] == 0
         assert p1.shape == (n, 38, h, w) and h1.shape == (n, 19, h, w)
