@@ -127,7 +127,15 @@ int launch_resize_cubic_f32(const float* src, int64_t sstride, int32_t pstride, 
 // source rows those output rows need -- once, instead of once per output row as resize_cubic_f32
 // does -- keeps them in its own LDS column, then makes every output row's vertical sum from them.
 // The f32 operations of each output element are resize_cubic_f32's (cv_cubic_f32), in its order.
-constexpr int kUpRows = 8, kUpSrc = 8;
+// Round 4: kUpRows and the prefetch (every source row's four taps loaded before the first
+// horizontal sum: one memory latency per block instead of one per source row) are build knobs.
+#ifndef UP_ROWS
+#define UP_ROWS 16
+#endif
+#ifndef UP_PREFETCH
+#define UP_PREFETCH 1
+#endif
+constexpr int kUpRows = UP_ROWS, kUpSrc = 8;
 __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restrict__ src, int64_t sstride, int pstride,
                                                            int64_t src_fstride, int sh, int sw, int cn,
                                                            float* __restrict__ dst, int64_t dst_fstride, int dh, int dw,
@@ -145,6 +153,27 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restri
 #pragma unroll
   for (int j = 0; j < 4; ++j) col[j] = (int64_t)clampc(tx.s - 1 + j, 0, sw - 1) * pstride;
   const float* fs = src + (int64_t)f * src_fstride + c;
+#if UP_PREFETCH
+  float q[kUpSrc][4];
+#pragma unroll
+  for (int r = 0; r < kUpSrc; ++r) {
+    if (r < nr) {
+      const float* row = fs + (int64_t)clampc(r0 + r, 0, sh - 1) * sstride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[r][j] = row[col[j]];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kUpSrc; ++r) {
+    if (r < nr) {
+      float h = __fmul_rn(q[r][0], tx.c[0]);
+      h = __fadd_rn(h, __fmul_rn(q[r][1], tx.c[1]));
+      h = __fadd_rn(h, __fmul_rn(q[r][2], tx.c[2]));
+      h = __fadd_rn(h, __fmul_rn(q[r][3], tx.c[3]));
+      hsum[r][threadIdx.x] = h;
+    }
+  }
+#else
   for (int r = 0; r < nr; ++r) {
     const float* row = fs + (int64_t)clampc(r0 + r, 0, sh - 1) * sstride;
     float h = __fmul_rn(row[col[0]], tx.c[0]);
@@ -153,6 +182,7 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restri
     h = __fadd_rn(h, __fmul_rn(row[col[3]], tx.c[3]));
     hsum[r][threadIdx.x] = h;
   }
+#endif
   const bool simd = x * cn + c < dw * cn / 4 * 4;
   float* o = dst + (int64_t)f * dst_fstride + ((int64_t)c * dh + y0) * dw + x;
   for (int y = y0; y <= ylast; ++y, o += dw) {
