@@ -9,6 +9,24 @@ namespace op {
 
 __device__ __forceinline__ float norm_u8(int v) { return __fsub_rn(__fdiv_rn((float)v, 255.0f), 0.5f); }
 
+// The cubic taps of output rows y0 .. y0 + TY - 1 (clamped to ylast), block-uniform: lane yy of the
+// wave makes row yy's (one f64 tap computation per lane instead of TY per lane) and v_readlane
+// moves them to scalar registers.  Lanes 0 .. TY-1 must be active (a lane that has returned holds
+// no defined value for v_readlane).
+template <int TY>
+__device__ __forceinline__ void row_taps(int y0, int ylast, double scy, CubicTap (&ty)[TY]) {
+  static_assert(TY <= 64, "one row per lane");
+  const int lane = threadIdx.x & 63;
+  const CubicTap t = cv_cubic_tap_s(min(y0 + min(lane, TY - 1), ylast), scy);
+#pragma unroll
+  for (int yy = 0; yy < TY; ++yy) {
+    ty[yy].s = __builtin_amdgcn_readlane(t.s, yy);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      ty[yy].c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.c[j]), yy));
+  }
+}
+
 // Padded network input (h = ph, w = pw, 1-pixel zero halo): pixel (x, y) < (rw, rh) is the cubic
 // resize of the frame, the rest the pad colour (104, 117, 123) (pose_detector.py:446, :46-55),
 // normalised (x/255 - 0.5, :426-431).  SPLIT: 16 channels as bf16 hi/lo (split format), else
@@ -144,11 +162,17 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restri
   const int x = blockIdx.x * 256 + threadIdx.x;
   const int y0 = blockIdx.y * kUpRows;
   const int f = blockIdx.z / cn, c = blockIdx.z - (blockIdx.z / cn) * cn;
-  if (x >= dw) return;  // no barrier below: a thread reads only its own LDS column
+  // no barrier below: a thread reads only its own LDS column; whole waves past the right edge
+  // leave (lanes 0 .. kUpRows-1 of a wave make its row taps)
+  if (blockIdx.x * 256 + (threadIdx.x & ~63) >= dw) return;
+  const bool live = x < dw;
   const int ylast = min(y0 + kUpRows - 1, dh - 1);
-  const int r0 = cv_cubic_tap_s(y0, scy).s - 1;
-  const int nr = cv_cubic_tap_s(ylast, scy).s + 2 - r0 + 1;  // <= kUpSrc (the launcher checks)
-  const CubicTap tx = cv_cubic_tap_s(x, scx);
+  // lane yy makes output row y0 + yy's taps (clamped to ylast); each row's are read out by
+  // v_readlane where they are used (kUpRows rows of taps would not fit the scalar registers)
+  const CubicTap tl = cv_cubic_tap_s(min(y0 + min((int)(threadIdx.x & 63), kUpRows - 1), ylast), scy);
+  const int r0 = __builtin_amdgcn_readlane(tl.s, 0) - 1;
+  const int nr = __builtin_amdgcn_readlane(tl.s, kUpRows - 1) + 2 - r0 + 1;  // <= kUpSrc (the launcher checks)
+  const CubicTap tx = cv_cubic_tap_s(min(x, dw - 1), scx);
   int64_t col[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) col[j] = (int64_t)clampc(tx.s - 1 + j, 0, sw - 1) * pstride;
@@ -183,24 +207,32 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restri
     hsum[r][threadIdx.x] = h;
   }
 #endif
+  // dead lanes (x >= dw) stay to the end: lanes 0 .. kUpRows-1 hold the row taps read below
   const bool simd = x * cn + c < dw * cn / 4 * 4;
   float* o = dst + (int64_t)f * dst_fstride + ((int64_t)c * dh + y0) * dw + x;
-  for (int y = y0; y <= ylast; ++y, o += dw) {
-    const CubicTap ty = cv_cubic_tap_s(y, scy);
-    const int b = ty.s - 1 - r0;
+#pragma unroll
+  for (int yy = 0; yy < kUpRows; ++yy) {
+    if (y0 + yy > ylast) break;
+    CubicTap ty1;
+    ty1.s = __builtin_amdgcn_readlane(tl.s, yy);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      ty1.c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tl.c[j]), yy));
+    const int b = ty1.s - 1 - r0;
     const float h0 = hsum[b][threadIdx.x], h1 = hsum[b + 1][threadIdx.x];
     const float h2 = hsum[b + 2][threadIdx.x], h3 = hsum[b + 3][threadIdx.x];
     float v;
     if (simd) {
-      const float t3 = __fmul_rn(h3, ty.c[3]);
-      const float t2 = __fadd_rn(__fmul_rn(h2, ty.c[2]), t3);
-      const float t1 = __fadd_rn(__fmul_rn(h1, ty.c[1]), t2);
-      v = __fadd_rn(__fmul_rn(h0, ty.c[0]), t1);
+      const float t3 = __fmul_rn(h3, ty1.c[3]);
+      const float t2 = __fadd_rn(__fmul_rn(h2, ty1.c[2]), t3);
+      const float t1 = __fadd_rn(__fmul_rn(h1, ty1.c[1]), t2);
+      v = __fadd_rn(__fmul_rn(h0, ty1.c[0]), t1);
     } else {
-      v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty.c[0]), __fmul_rn(h1, ty.c[1])), __fmul_rn(h2, ty.c[2])),
-                    __fmul_rn(h3, ty.c[3]));
+      v = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h0, ty1.c[0]), __fmul_rn(h1, ty1.c[1])),
+                              __fmul_rn(h2, ty1.c[2])),
+                    __fmul_rn(h3, ty1.c[3]));
     }
-    *o = v;
+    if (live) o[(int64_t)yy * dw] = v;
   }
 }
 
@@ -364,30 +396,33 @@ int launch_resize_cubic_f32_planar_mean(const CubicMeanArgs& a, float* dst, int3
 template <int G, int TY>
 __global__ __launch_bounds__(256, ROWS_MINB) void resize_cubic_f32_planar_mean_rows(CubicMeanArgs a, float* __restrict__ dst,
                                                                          int64_t dst_fstride, int dh, int dw, int npaf,
-                                                                         int nheat, int ngroups, int rcap) {
+                                                                         int nheat, int ngroups, int rcap, int nbx,
+                                                                         int nby, int nblocks) {
   extern __shared__ float hsl[];  // [rcap][256], each thread its own column
-  const int tid = threadIdx.x, x = blockIdx.x * 256 + tid;
-  const int y0 = blockIdx.y * TY;
-  const int f = blockIdx.z / ngroups, c0 = (blockIdx.z - f * ngroups) * G;
-  if (x >= dw) return;
+  // XCD-aware order: XCD k (= linear id mod 8) runs the k-th eighth of the (x, y, channel, frame)
+  // blocks in order, so the blocks of neighbouring output rows -- which read the same source rows
+  // -- share one L2 (round-robin placement put them on different XCDs: 1.76x the maps' bytes)
+  const int per = (nblocks + 7) >> 3;
+  const int lb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (lb >= nblocks) return;
+  const int bz = lb / (nbx * nby), rem = lb - bz * nbx * nby;
+  const int by = rem / nbx, bx = rem - by * nbx;
+  const int tid = threadIdx.x, x0 = bx * 256, x = x0 + tid;
+  const int y0 = by * TY;
+  const int f = bz / ngroups, c0 = (bz - f * ngroups) * G;
+  if (x0 + (tid & ~63) >= dw) return;  // whole waves past the right edge only (lanes 0..TY-1 make row taps)
+  const bool live = x < dw;
   const int nch = npaf + nheat;
   const int ylast = min(y0 + TY - 1, dh - 1);
   float sum[G][TY];
   for (int k = 0; k < a.ns; ++k) {
     const int sh = a.sh[k], sw = a.sw[k];
-    const int r0 = cv_cubic_tap_s(y0, a.scy[k]).s - 1;
-    const int nr = cv_cubic_tap_s(ylast, a.scy[k]).s + 2 - r0 + 1;
+    CubicTap ty[TY];  // block-uniform: scalar registers
+    row_taps<TY>(y0, ylast, a.scy[k], ty);
+    const int r0 = ty[0].s - 1;                   // row y0's first tap
+    const int nr = ty[TY - 1].s + 2 - r0 + 1;     // .. row ylast's last
     const bool fits = nr <= rcap;  // never false (host bound); else the outputs are NaN
-    CubicTap ty[TY];  // block-uniform: moved to scalar registers
-#pragma unroll
-    for (int yy = 0; yy < TY; ++yy) {
-      const CubicTap t = cv_cubic_tap_s(min(y0 + yy, ylast), a.scy[k]);
-      ty[yy].s = __builtin_amdgcn_readfirstlane(t.s);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        ty[yy].c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t.c[j])));
-    }
-    const CubicTap tx = cv_cubic_tap_s(x, a.scx[k]);
+    const CubicTap tx = cv_cubic_tap_s(min(x, dw - 1), a.scx[k]);
     int col[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) col[j] = clampc(tx.s - 1 + j, 0, sw - 1);
@@ -431,6 +466,7 @@ __global__ __launch_bounds__(256, ROWS_MINB) void resize_cubic_f32_planar_mean_r
       }
     }
   }
+  if (!live) return;
   const int64_t plane = (int64_t)dh * dw;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -470,9 +506,15 @@ int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst,
     attr = true;
   }
   const int ngroups = (npaf + nheat + G - 1) / G;
-  hipLaunchKernelGGL((resize_cubic_f32_planar_mean_rows<G, TY>),
-                     dim3((unsigned)((dw + 255) / 256), (unsigned)((dh + TY - 1) / TY), (unsigned)(n * ngroups)),
-                     dim3(256), lds, st, a, dst, dst_fstride, dh, dw, npaf, nheat, ngroups, rcap);
+  const int nbx = (dw + 255) / 256, nby = (dh + TY - 1) / TY;
+  const int64_t nb = (int64_t)nbx * nby * n * ngroups;
+  if (nb > INT32_MAX - 8) {
+    set_error("resize_cubic_f32_planar_mean_rows: grid too large");
+    return OP_ERR_INVALID;
+  }
+  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
+  hipLaunchKernelGGL((resize_cubic_f32_planar_mean_rows<G, TY>), dim3(grid), dim3(256), lds, st, a, dst, dst_fstride,
+                     dh, dw, npaf, nheat, ngroups, rcap, nbx, nby, (int)nb);
   OP_AFTER_LAUNCH("resize_cubic_f32_planar_mean_rows", st);
   OP_HIP_CHECK(hipGetLastError());
   *taken = true;
@@ -512,14 +554,7 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_planar_mean_tile(CubicMe
     const int nc = clampc(cv_cubic_tap_s(xl, a.scx[k]).s + 2, 0, sw - 1) - cx0 + 1;
     const bool fits = nr <= rcap && nc <= ccap;  // never false (host bounds); else the outputs are NaN
     CubicTap ty[TY];  // block-uniform: scalar registers
-#pragma unroll
-    for (int yy = 0; yy < TY; ++yy) {
-      const CubicTap t = cv_cubic_tap_s(min(y0 + yy, ylast), a.scy[k]);
-      ty[yy].s = __builtin_amdgcn_readfirstlane(t.s);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        ty[yy].c[j] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t.c[j])));
-    }
+    row_taps<TY>(y0, ylast, a.scy[k], ty);
     const CubicTap tx = cv_cubic_tap_s(xc, a.scx[k]);
     int col[4];
 #pragma unroll
