@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void resize_cubic_f32_up(const float* __restri
   float* o = dst + (int64_t)f * dst_fstride + ((int64_t)c * dh + y0) * dw + x;
 #pragma unroll
   for (int yy = 0; yy < kUpRows; ++yy) {
-    if (y0 + yy > ylast) break;
+    if (y0 + yy > ylast) continue;  // (not break: the loop stays unrolled, constant readlane lanes)
     CubicTap ty1;
     ty1.s = __builtin_amdgcn_readlane(tl.s, yy);
 #pragma unroll
@@ -482,23 +482,21 @@ __global__ __launch_bounds__(256, ROWS_MINB) void resize_cubic_f32_planar_mean_r
 #define MEAN_ROWS_G 1
 #endif
 #ifndef MEAN_ROWS_TY
-#define MEAN_ROWS_TY 8
+#define MEAN_ROWS_TY 12
 #endif
-int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
-                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
-                                             bool* taken) {
-  constexpr int G = MEAN_ROWS_G, TY = MEAN_ROWS_TY;
+// One launch of the row-block form with TY output rows per block; *taken false when a scale's
+// rows exceed the 64-KiB LDS budget.
+template <int TY>
+static int mean_rows_ty(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n, int32_t dh, int32_t dw,
+                        int32_t npaf, int32_t nheat, hipStream_t st, bool* taken) {
+  constexpr int G = MEAN_ROWS_G;
   *taken = false;
-  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
-    set_error("resize_cubic_f32_planar_mean_rows: 1..OP_MAX_SCALES scales");
-    return OP_ERR_INVALID;
-  }
   // rows TY consecutive outputs read: floor((TY - 1) * s) + 1 distinct tap origins + 3, + 1 for
   // the f32 rounding of the source coordinate, + 1 spare (as fused_lds)
   int rcap = 0;
   for (int k = 0; k < a.ns; ++k) rcap = std::max(rcap, (int)std::floor((TY - 1) * a.scy[k]) + 7);
   const size_t lds = (size_t)rcap * 256 * sizeof(float);
-  if (lds > 64 * 1024) return OP_OK;  // caller runs resize_cubic_f32_planar_mean
+  if (lds > 64 * 1024) return OP_OK;
   static bool attr = false;
   if (!attr) {
     OP_HIP_CHECK(hipFuncSetAttribute((const void*)resize_cubic_f32_planar_mean_rows<G, TY>,
@@ -519,6 +517,22 @@ int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst,
   OP_HIP_CHECK(hipGetLastError());
   *taken = true;
   return OP_OK;
+}
+
+// MEAN_ROWS_TY (12) rows per block, or 8 where a scale's second resize shrinks its crop so much
+// that 12 rows' source rows exceed the LDS budget (small frames: ~7.7x at 96x128); *taken false
+// when neither fits (the caller runs the per-frame form).
+int launch_resize_cubic_f32_planar_mean_rows(const CubicMeanArgs& a, float* dst, int64_t dst_fstride, int32_t n,
+                                             int32_t dh, int32_t dw, int32_t npaf, int32_t nheat, hipStream_t st,
+                                             bool* taken) {
+  *taken = false;
+  if (a.ns < 1 || a.ns > OP_MAX_SCALES) {
+    set_error("resize_cubic_f32_planar_mean_rows: 1..OP_MAX_SCALES scales");
+    return OP_ERR_INVALID;
+  }
+  const int rc = mean_rows_ty<MEAN_ROWS_TY>(a, dst, dst_fstride, n, dh, dw, npaf, nheat, st, taken);
+  if (rc || *taken || MEAN_ROWS_TY == 8) return rc;
+  return mean_rows_ty<8>(a, dst, dst_fstride, n, dh, dw, npaf, nheat, st, taken);
 }
 
 // The row-block second pass with each scale's source tile staged in LDS: the block's nr source
