@@ -338,54 +338,12 @@ def batch1_line(L, ctx, low, FH, FW, steps=60, warmup=10):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=None,
-                    help="frames per step per GPU; default 232 for the 368x368 headline, 64 for 1280x720 single "
-                         "scale (756 7x7 workgroups, 2.95 rounds; 981-989 -> 991-995 frames/s over 63 in an "
-                         "interleaved A/B, profiles/r03/ab_r03_c5_batch_63_64.log), 16 for --precise.  232: the 7x7 kernel's 640-pixel raster tiles, "
-                         "232 x 2116 / 640 = 767.05 -> 768 per branch x 2 = 1536 workgroups = six full rounds of "
-                         "one per CU (114 frames left 14 CUs idle in its third round); interleaved A/B "
-                         "1818-1824 / 1827-1835 / 1847-1849 frames/s at 114 / 116 / 232, "
-                         "profiles/r03/ab_r03_batch_114_116_232.log")
-    ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
-                    help="post-process input: COCO-like multi-person maps (default) or the random-weight "
-                         "network's own last stage")
-    ap.add_argument("--cpu-frames", type=int, default=5)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-variants", action="store_true", help="skip the network-maps / fp32 side lines")
-    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
-    ap.add_argument("--graph", type=int, default=0, help="1: replay each step as one captured hipGraph")
-    ap.add_argument("--precision", choices=["bf16x3", "fp32"], default="bf16x3",
-                    help="conv arithmetic: 3xBF16-split products (f32 accumulate) or exact f32 MFMA")
-    ap.add_argument("--frame", default="368x368",
-                    help="HxW of the synthetic frames (BASELINE configs: 368x368 = C2/C3, the default "
-                         "and the headline; 720x1280 = C5's 720p stream, single scale)")
-    ap.add_argument("--precise", action="store_true",
-                    help="C4: multi-scale detect_precise (4 scales, cubic resizes) on the staged batch "
-                         "(op_run_staged_precise: one batched forward per scale)")
-    args = ap.parse_args()
+def bench_line(args, L, Wm, Fr, transport, rank, world, local):
+    """One configuration (args.frame / args.precise / args.batch) on this rank: context, gather and
+    step loop, the timed steps, the per-class breakdown and the roofline; returns the JSON fields
+    and the live state (close_line frees it)."""
     FH, FW = (int(v) for v in args.frame.lower().split("x"))
     headline = (FH, FW) == (368, 368) and not args.precise
-    if not headline:
-        args.no_cpu_baseline = True
-        args.no_variants = True
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("OP_BENCH_DEVICE"):  # rehearsal aid: every rank on one device (RCCL then refuses
-        local = int(os.environ["OP_BENCH_DEVICE"])  # the duplicate GPU and the labelled TCP gather runs)
-    import importlib
-    L = importlib.import_module(PKG + "._lib")
-    Wm = importlib.import_module(PKG + ".weights")
-    Fr = importlib.import_module(PKG + ".frames")
-    transport = Fr.SocketTransport(rank, world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                                   timeout=300.0)  # world 1: no sockets; bootstrap of the 1-rank gather
-
     if args.batch is None:  # three rounds of full-chip 7x7 launches per step (single scale); C4: 16 frames
         args.batch = 16 if args.precise else (232 if (FH, FW) == (368, 368) else 64)
     B = args.batch
@@ -492,6 +450,96 @@ def main():
                          "between kernels)" % n_extra,
         "roofline": roofline,
     }
+    # the whole step against the same peak: every conv FLOP of the step / the step's wall time
+    step_tf = out["gflop_per_frame"] * 1e9 * frames_total / elapsed / 1e12
+    out["step_tflops"] = round(step_tf, 2)
+    out["step_frac_of_peak"] = round(step_tf / (BF16_DENSE_PEAK_TFLOPS / 3.0 if args.precision == "bf16x3"
+                                                else FP32_MATRIX_PEAK_TFLOPS), 4)
+    return out, {"ctx": ctx, "run": run, "gather": gather, "low": low, "B": B, "FH": FH, "FW": FW}
+
+
+def close_line(st):
+    st["run"].close()
+    g = st["gather"]
+    if g.g is not None and g.device:
+        g.g.close()
+    st["ctx"].close()
+
+
+SIDE_KEYS = ("value", "unit", "metric", "ms_per_step", "steps", "warmup", "config", "gflop_per_frame",
+             "persons_per_s", "frames_over_caps", "frames_overflow", "stage_ms_per_step", "stage_ms_sum",
+             "roofline", "step_tflops", "step_frac_of_peak")
+
+
+def side_line(args, frame, precise, L, Wm, Fr, transport, local):
+    """Another BASELINE config measured by this same run (world 1): a fresh context of its own, the
+    same step loop and fields as `python bench.py --frame FRAME [--precise]` (its default batch)."""
+    a = argparse.Namespace(**vars(args))
+    a.frame, a.precise, a.batch, a.maps, a.graph = frame, precise, None, "synthetic", 0
+    a.no_variants = a.no_cpu_baseline = True
+    a.steps = args.side_steps or args.steps
+    t0 = time.perf_counter()
+    o, st = bench_line(a, L, Wm, Fr, transport, 0, 1, local)
+    close_line(st)
+    line = {k: o[k] for k in SIDE_KEYS if k in o}
+    line["wall_s"] = round(time.perf_counter() - t0, 2)  # setup (weights, arenas) + warm-up + timed + profiled steps
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step per GPU; default 232 for the 368x368 headline, 64 for 1280x720 single "
+                         "scale (756 7x7 workgroups, 2.95 rounds; 981-989 -> 991-995 frames/s over 63 in an "
+                         "interleaved A/B, profiles/r03/ab_r03_c5_batch_63_64.log), 16 for --precise.  232: the 7x7 kernel's 640-pixel raster tiles, "
+                         "232 x 2116 / 640 = 767.05 -> 768 per branch x 2 = 1536 workgroups = six full rounds of "
+                         "one per CU (114 frames left 14 CUs idle in its third round); interleaved A/B "
+                         "1818-1824 / 1827-1835 / 1847-1849 frames/s at 114 / 116 / 232, "
+                         "profiles/r03/ab_r03_batch_114_116_232.log")
+    ap.add_argument("--maps", choices=["synthetic", "network"], default="synthetic",
+                    help="post-process input: COCO-like multi-person maps (default) or the random-weight "
+                         "network's own last stage")
+    ap.add_argument("--cpu-frames", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the network-maps / fp32 side lines")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--no-side-lines", action="store_true",
+                    help="skip the C5 720p and C4 multi-scale lines of the default run (variants)")
+    ap.add_argument("--side-steps", type=int, default=None, help="timed steps of each side line (default: --steps)")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay each step as one captured hipGraph")
+    ap.add_argument("--precision", choices=["bf16x3", "fp32"], default="bf16x3",
+                    help="conv arithmetic: 3xBF16-split products (f32 accumulate) or exact f32 MFMA")
+    ap.add_argument("--frame", default="368x368",
+                    help="HxW of the synthetic frames (BASELINE configs: 368x368 = C2/C3, the default "
+                         "and the headline; 720x1280 = C5's 720p stream, single scale)")
+    ap.add_argument("--precise", action="store_true",
+                    help="C4: multi-scale detect_precise (4 scales, cubic resizes) on the staged batch "
+                         "(op_run_staged_precise: one batched forward per scale)")
+    args = ap.parse_args()
+    FH, FW = (int(v) for v in args.frame.lower().split("x"))
+    headline = (FH, FW) == (368, 368) and not args.precise
+    if not headline:
+        args.no_cpu_baseline = True
+        args.no_variants = True
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("OP_BENCH_DEVICE"):  # rehearsal aid: every rank on one device (RCCL then refuses
+        local = int(os.environ["OP_BENCH_DEVICE"])  # the duplicate GPU and the labelled TCP gather runs)
+    import importlib
+    L = importlib.import_module(PKG + "._lib")
+    Wm = importlib.import_module(PKG + ".weights")
+    Fr = importlib.import_module(PKG + ".frames")
+    transport = Fr.SocketTransport(rank, world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                                   timeout=300.0)  # world 1: no sockets; bootstrap of the 1-rank gather
+
+    out, st = bench_line(args, L, Wm, Fr, transport, rank, world, local)
+    ctx, run, gather, low, B = st["ctx"], st["run"], st["gather"], st["low"], st["B"]
+    cpu_frames = None
     if not args.no_variants and world == 1:
         # side lines (not `value`): the same workload with the network's own maps, and in exact f32
         variants = {}
@@ -548,16 +596,24 @@ def main():
         ctx.set_precision(args.precision)
         # single-image latency (BASELINE config 2 names one 368x368 frame): last, it re-stages
         variants["batch1"] = batch1_line(L, ctx, low, FH, FW)
+        cpu_frames = run.pool[0].array[:4].copy()
+        close_line(st)
+        st = None
+        # the other BASELINE configs on the same box in the same run (their own contexts): C5's 720p
+        # stream shape, single scale (pose_detector.py:484-517), and C4's 4-scale detect_precise
+        # (:433-482) on 1280x720 frames
+        if not args.no_side_lines:
+            variants["c5_720p"] = side_line(args, "720x1280", False, L, Wm, Fr, transport, local)
+            variants["c4_precise"] = side_line(args, "720x1280", True, L, Wm, Fr, transport, local)
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        frames = run.pool[0].array[:4].copy()
-        out["cpu_baseline"] = cpu_baseline(frames, low, args.cpu_frames)
+        if cpu_frames is None:
+            cpu_frames = run.pool[0].array[:4].copy()
+        out["cpu_baseline"] = cpu_baseline(cpu_frames, low, args.cpu_frames)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    run.close()
-    if gather.g is not None and gather.device:
-        gather.g.close()
-    ctx.close()
+    if st is not None:
+        close_line(st)
     if transport:
         transport.close()
 

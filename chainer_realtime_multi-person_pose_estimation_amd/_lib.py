@@ -20,7 +20,7 @@ N_JOINTS, N_LIMBS, N_PAF, N_HEAT, N_LAYERS = 18, 19, 38, 19, 92
 
 # Every symbol include/openpose_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "op_last_error", "op_default_params", "op_default_limits", "op_layer_info", "op_create", "op_destroy",
+    "op_last_error", "op_build_info", "op_default_params", "op_default_limits", "op_layer_info", "op_create", "op_destroy",
     "op_set_weights", "op_detect", "op_preprocess", "op_forward", "op_forward_stages", "op_resize_images", "op_compute_peaks",
     "op_compute_connections", "op_grouping", "op_postprocess", "op_stage_frames", "op_stage_maps",
     "op_use_staged_maps", "op_run_staged", "op_run_staged_graph", "op_graph_info", "op_synchronize", "op_fetch_result",
@@ -78,6 +78,7 @@ def lib():
     P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     sig = {
         "op_last_error": ([], ctypes.c_char_p),
+        "op_build_info": ([ctypes.c_char_p, I32], ctypes.c_int),
         "op_default_params": ([P], ctypes.c_int),
         "op_default_limits": ([P], ctypes.c_int),
         "op_layer_info": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), P, P, P], ctypes.c_int),
@@ -157,6 +158,33 @@ def lib():
     return L
 
 
+def build_info():
+    """The source digest baked into the loaded library at build time ("sha256:<hex>")."""
+    buf = ctypes.create_string_buffer(96)
+    check(lib().op_build_info(buf, len(buf)), "op_build_info")
+    return buf.value.decode("ascii")
+
+
+def source_digest(csrc=None):
+    """The same digest recomputed from the checked-out sources (csrc/Makefile DIGEST_SRCS: sha256
+    of the `sha256sum` listing of csrc/*.hip *.hpp *.cpp, csrc/Makefile and include/*.h, paths as
+    written relative to csrc/, in sorted order); None when the sources are not present."""
+    import glob
+    import hashlib
+    csrc = csrc or os.path.join(_HERE, "csrc")
+    if not os.path.isfile(os.path.join(csrc, "Makefile")):
+        return None
+    names = ["Makefile"]
+    for pat in ("*.hip", "*.hpp", "*.cpp"):
+        names += [os.path.basename(p) for p in glob.glob(os.path.join(csrc, pat))]
+    names += ["../../include/" + os.path.basename(p) for p in glob.glob(os.path.join(csrc, "..", "..", "include", "*.h"))]
+    listing = ""
+    for n in sorted(names, key=lambda v: v.encode()):
+        with open(os.path.join(csrc, n), "rb") as f:
+            listing += "%s  %s\n" % (hashlib.sha256(f.read()).hexdigest(), n)
+    return "sha256:" + hashlib.sha256(listing.encode()).hexdigest()
+
+
 def last_error():
     return (lib().op_last_error() or b"").decode("utf-8", "replace")
 
@@ -223,7 +251,7 @@ CENSUS = {"7x7_splitk": 11, "7x7_other": 12, "3x3_w48": 13, "3x3_w32": 14, "3x3_
           "3x3_big": 17, "conv1_pair": 18, "3x3_r256": 19, "3x3_r128": 20, "3x3_r_pool": 21,
           "7x7_planar": 22, "7x7_frame_aligned": 23, "7x7_tight": 24,
           "cubic_fused": 25, "cubic_two_pass": 26,
-          "splitk_inkernel": 27, "cubic_rows": 28}
+          "cubic_rows": 28}
 CENSUS_SLOTS = 32
 
 

@@ -421,9 +421,7 @@ struct SplitkWs {
   size_t floats = 0;
   size_t short_by = 0;  // largest request refused during capture
   std::vector<float*> retired;  // outgrown buffers: a graph captured earlier may still read them
-  int32_t* cnt = nullptr;       // kSplitkCounters zeroed arrival counters (BigTiling::cnt)
 };
-constexpr int kSplitkCounters = 1 << 16;
 static std::mutex g_ws_mu;
 static std::map<hipStream_t, SplitkWs> g_ws;
 
@@ -436,35 +434,12 @@ static float* splitk_ws(hipStream_t st, size_t floats) {
     e.short_by = std::max(e.short_by, floats);
     return nullptr;
   }
-  if (!e.cnt) {  // allocated with the first workspace, outside capture; kept for the stream's life
-    int32_t* c = nullptr;
-    if (hipMalloc(&c, kSplitkCounters * sizeof(int32_t)) != hipSuccess) return nullptr;
-    if (hipMemset(c, 0, kSplitkCounters * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(c);
-      return nullptr;
-    }
-    e.cnt = c;
-  }
   float* p = nullptr;
   if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
   if (e.p) e.retired.push_back(e.p);
   e.p = p;
   e.floats = floats;
   return p;
-}
-
-// The stream's arrival counters when a launch of `tiles` (weight set, pixel tile) pairs finishes
-// its split-K in the conv kernel -- OFF by default, OP_SPLITK_INKERNEL=1 selects it: one frame's
-// 368x368 call measured 3.03 ms per frame against 1.95 with the reduce launches
-// (profiles/r04/ab_r04l_splitk_inkernel_sc1.log).  The last arriver of a tile reads all S partials
-// of the tile alone: 22-44 CUs pull the launch's 17 MB of partials at one CU's bandwidth each, where
-// conv_m16_splitk_reduce spreads the same bytes over the whole chip in 6.4 us.
-static int32_t* splitk_counters(hipStream_t st, int64_t tiles) {
-  const char* e = getenv("OP_SPLITK_INKERNEL");  // read per launch: the parity test A/Bs it in-process
-  if (!(e && atoi(e) == 1) || tiles > kSplitkCounters) return nullptr;
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  auto it = g_ws.find(st);
-  return it == g_ws.end() ? nullptr : it->second.cnt;
 }
 
 size_t splitk_ws_capture_short(hipStream_t st) {
@@ -490,7 +465,6 @@ void splitk_ws_release(hipStream_t st) {
   auto it = g_ws.find(st);
   if (it == g_ws.end()) return;
   if (it->second.p) (void)hipFree(it->second.p);
-  if (it->second.cnt) (void)hipFree(it->second.cnt);
   for (float* p : it->second.retired) (void)hipFree(p);
   g_ws.erase(it);
 }
@@ -506,7 +480,7 @@ __global__ __launch_bounds__(256) void conv_m16_splitk_reduce(SplitConvShape s, 
   if (i >= (int64_t)tl.total * q) return;
   const int P = (int)(i / q), co = (int)(i - (int64_t)P * q) * 4;
   if (co >= g.cout_store) return;
-  splitk_reduce_item<false>(s, g, grp, tl, max(g0.cop, g1.cop), P, co);
+  splitk_reduce_item(s, g, grp, tl, max(g0.cop, g1.cop), P, co);
 }
 
 // Split-K partials of a conv with the fused 2x2 max-pool (round 4: pooled 3x3 launches that fill
@@ -775,7 +749,6 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   BigTiling t = tl;
   t.ksplit = 1;
   t.ws = nullptr;
-  t.cnt = nullptr;
   static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
   if (s.splitk && (!pool || s.groups == 1)) {
     const int pairs = s.c16 / 2;
@@ -797,14 +770,12 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
       if (ws) {
         t.ksplit = S;
         t.ws = ws;
-        if (!pool) t.cnt = splitk_counters(st, (int64_t)t.units * t.per_unit);
       }
     }
   }
   const dim3 grid(blocks, (unsigned)t.ksplit);
   census_add(pool ? OP_CENSUS_3X3_POOL : tl.tc == 48 ? OP_CENSUS_3X3_W48 : OP_CENSUS_3X3_W32);
   if (t.ksplit > 1) census_add(OP_CENSUS_3X3_SPLITK);
-  if (t.cnt) census_add(OP_CENSUS_SPLITK_INKERNEL);
   if (pool)
     hipLaunchKernelGGL(conv_m16k_bf16x3<true>, grid, dim3(256), lds, st, s, g[0], g1, t);
   else if (tl.tc == 48) {
@@ -817,7 +788,7 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
     const int64_t items = (int64_t)s.n * (s.h / 2) * (s.w / 2) * (g[0].cop / 4);
     hipLaunchKernelGGL(conv_m16_splitk_reduce_pool, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, s, g[0], t);
     OP_AFTER_LAUNCH("conv_m16_splitk_reduce_pool", st);
-  } else if (t.ksplit > 1 && !t.cnt) {
+  } else if (t.ksplit > 1) {
     int cop_max = g[0].cop;
     if (s.groups > 1) cop_max = std::max(cop_max, g[1].cop);
     const int64_t items = (int64_t)t.total * (cop_max / 4);
@@ -1022,26 +993,23 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
       *taken = 1;
       tl.ksplit = 1;
       tl.ws = nullptr;
-      tl.cnt = nullptr;
       if (S > kMaxSplitK) S = 1;  // the reduce's unrolled partial loads
       if (s.splitk && S > 1) {
         float* ws = splitk_ws(st, (size_t)S * s.groups * tl.total * cop_max);
         if (ws) {
           tl.ksplit = S;
           tl.ws = ws;
-          tl.cnt = splitk_counters(st, (int64_t)tl.units * tl.per_unit);
         }
       }
       const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
       census_add(npx);
       if (tl.ksplit > 1) census_add(OP_CENSUS_7X7_SPLITK);
-      if (tl.cnt) census_add(OP_CENSUS_SPLITK_INKERNEL);
       if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
       if (tl.fa_tiles) census_add(OP_CENSUS_7X7_FRAME_ALIGNED);
       if (tl.pitch == s.w + 6) census_add(OP_CENSUS_7X7_TIGHT);
       const int rc = launch_m16_7x7(npx, st, s, g[0], g1, tl);
       if (rc != OP_OK) return rc;
-      if (tl.ksplit > 1 && !tl.cnt) {
+      if (tl.ksplit > 1) {
         OP_AFTER_LAUNCH("conv_m16_bf16x3", st);
         const int64_t items = (int64_t)tl.total * (cop_max / 4);
         hipLaunchKernelGGL(conv_m16_splitk_reduce, dim3((unsigned)((items + 255) / 256), (unsigned)s.groups), dim3(256),

@@ -29,8 +29,6 @@ struct BigTiling {
                              // [x*per_xcd, (x+1)*per_xcd) for every weight set, sets adjacent
   int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
   float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
-  int32_t* cnt;              // non-null: split-K finished in the conv kernel (splitk_arrive), one
-                             // arrival counter per (weight set, pixel tile), zero between launches
   const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
 };
 
@@ -86,57 +84,24 @@ __device__ __forceinline__ void store_split_group(char* optr, int co, int kg, in
   }
 }
 
-// Split-K hand-off inside a launch (round 4 experiment, opt-in OP_SPLITK_INKERNEL=1: slower, see
-// splitk_counters in conv_big.hip): the split workgroups of a tile
-// write their f32 partials WRITE-THROUGH (`sc1`: 8-B agent-scope relaxed stores, no L2 copy), each
-// storing wave drains them (vmcnt(0)), the workgroup barrier, then ONE lane adds to the tile's
-// counter (agent-scope relaxed atomic); the workgroup whose add returns nsplit - 1 arrived last and
-// reads every partial with `sc1` loads (bypassing its CU's L1) -- the hand-off form of
-// MI355X_MICROARCH.md's visibility table (row 1: no release fence, no acquire).  An agent-scope
-// release fence in its place writes back the whole XCD L2 per workgroup: measured 1.96 -> 3.04 ms
-// per frame (profiles/r04/ab_r04k_splitk_inkernel_release_fence.log).
-typedef float floatx2g __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) int gi32_t;
-
-__device__ __forceinline__ void store_partial_sc1(float* p, const floatx4& v) {
-  gu64_t* q = (gu64_t*)p;
-  __hip_atomic_store(q, __builtin_bit_cast(unsigned long long, floatx2g{v[0], v[1]}), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, __builtin_bit_cast(unsigned long long, floatx2g{v[2], v[3]}), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool SC1>
-__device__ __forceinline__ floatx4 load_partial(const float* p) {
-  if constexpr (SC1) {
-    gu64_t* q = (gu64_t*)p;
-    const floatx2g a = __builtin_bit_cast(floatx2g, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const floatx2g b = __builtin_bit_cast(floatx2g, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    return floatx4{a[0], a[1], b[0], b[1]};
-  } else {
-    return *(const floatx4*)p;
-  }
-}
-
 // One (pixel P of the batch, 4 channels co..co+3) of a split-K conv: the tl.ksplit f32 partials
 // summed in split order onto the bias, the activation, and the split hi/lo (+ dense f32) store of
-// the kernels' own epilogue.  conv_m16_splitk_reduce runs it per thread (SC1 = false: a launch
-// boundary orders it after the conv); with tl.cnt the tile's last split runs it over the tile
-// (SC1: the partials handed off inside the launch).  Same arithmetic, same order: bit-identical.
+// the kernels' own epilogue; conv_m16_splitk_reduce runs it per thread (a launch boundary orders it
+// after the conv).  Round 5: the round-4 experiment that finished split-K inside the conv kernel
+// (last arriver at an agent-scope counter; measured slower, and its hand-off had no release /
+// acquire pairing -- advisor r04) is removed.
 // Round 4: every partial is loaded before the first add (a predicated, fully unrolled loop over at
 // most kMaxSplitK splits), so a thread waits for memory once instead of once per split (the
 // launch's 8 dependent load latencies were most of a one-frame reduce's 6.4 us); the adds keep
 // the split order.
 constexpr int kMaxSplitK = 16;
-template <bool SC1>
 __device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, const SplitConvGroup& g, int grp,
                                                    const BigTiling& tl, int wsc, int64_t P, int co) {
   floatx4 part[kMaxSplitK];
 #pragma unroll
   for (int sp = 0; sp < kMaxSplitK; ++sp)
     if (sp < tl.ksplit)
-      part[sp] = load_partial<SC1>(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
+      part[sp] = *(const floatx4*)(tl.ws + (((int64_t)sp * s.groups + grp) * tl.total + P) * wsc + co);
   floatx4 v = *(const floatx4*)(g.bias + co);
 #pragma unroll
   for (int sp = 0; sp < kMaxSplitK; ++sp)
@@ -163,30 +128,6 @@ __device__ __forceinline__ void splitk_reduce_item(const SplitConvShape& s, cons
   *(u16x4g*)d = vh;
   *(u16x4g*)(d + out_pc) = vl;
   if (g.out32) *(floatx4*)(g.out32 + ((int64_t)(f * s.h + y) * s.w + x) * s.cs_out32 + g.out32_off + co) = v;
-}
-
-// Called by every thread of a split's workgroup after its sc1 partial stores; true in the workgroup
-// that arrives last at *cnt (which it resets to zero for the next launch).  ACQUIRE: that workgroup
-// also runs one agent-scope acquire before its loads (kernels with more than one workgroup per CU,
-// outside the measured row).  `lds_word`: 4 B of LDS no wave reads any more.
-template <bool ACQUIRE>
-__device__ __forceinline__ bool splitk_arrive(int32_t* cnt, int nsplit, char* lds_word) {
-  __attribute__((address_space(3))) volatile int* flag = (__attribute__((address_space(3))) volatile int*)lds_word;
-  wait_vmcnt<0>();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    gi32_t* c = (gi32_t*)cnt;
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == nsplit - 1;
-    if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ACQUIRE && last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      wait_vmcnt<0>();
-    }
-    *flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  return *flag != 0;
 }
 
 // conv_m16.hip: launch conv_m16_bf16x3<7, npx, deep> on a raster tiling made by conv_big.hip (picks

@@ -241,18 +241,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-          if (co < g.cop) {
-            if (tl.cnt) store_partial_sc1(wsg + (int64_t)P * wsc + co, acc[cb][pb]);
-            else *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
-          }
-        }
-      }
-      // the tile's last split to finish sums all of them (no conv_m16_splitk_reduce launch)
-      if (tl.cnt && splitk_arrive<false>(tl.cnt + (unit * tl.per_unit + widx), nsplit, lds)) {
-        const int np = T.P1 - T.P0 + 1;
-        for (int i = threadIdx.x; i < np * (CW / 4); i += 512) {
-          const int P = T.P0 + i / (CW / 4), co = co0 + (i % (CW / 4)) * 4;
-          if (co < g.cout_store) splitk_reduce_item<true>(s, g, grp, tl, wsc, P, co);
+          if (co < g.cop) *(floatx4*)(wsg + (int64_t)P * wsc + co) = acc[cb][pb];
         }
       }
     } else {

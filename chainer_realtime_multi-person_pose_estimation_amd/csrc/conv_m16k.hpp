@@ -184,21 +184,7 @@ __global__ __launch_bounds__(256, 2) void conv_m16k_bf16x3(SplitConvShape s, Spl
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int co = co0 + ch * 64 + cb * 16 + 4 * kg;
-        if (co < g.cop) {
-          if (!POOL && tl.cnt) store_partial_sc1(wsg + P * wsc + co, acc[cb][pb]);
-          else *(floatx4*)(wsg + P * wsc + co) = acc[cb][pb];
-        }
-      }
-    }
-    // the tile's last split to finish sums all of them (no conv_m16_splitk_reduce launch)
-    // two workgroups per CU: outside the measured sc1-only row, so the last arriver also acquires
-    if (!POOL && tl.cnt && splitk_arrive<true>(tl.cnt + (unit * tl.per_unit + widx), nsplit, lds)) {
-      const int np = rows_here * cols_here;
-      for (int i = threadIdx.x; i < np * (CW / 4); i += 256) {
-        const int pix = i / (CW / 4), co = co0 + (i % (CW / 4)) * 4;
-        const int r = pix / cols_here, c = pix - r * cols_here;
-        const int64_t P = ((int64_t)frame * s.h + y0 + r) * s.w + x0 + c;
-        if (co < g.cout_store) splitk_reduce_item<true>(s, g, grp, tl, wsc, P, co);
+        if (co < g.cop) *(floatx4*)(wsg + P * wsc + co) = acc[cb][pb];
       }
     }
     return;

@@ -788,12 +788,14 @@ __device__ __forceinline__ bool may_reach(float v, float thresh) {
 // joint of frames x, x + 8, ...: the 18 joints' blocks of a frame read the same low-res pixel
 // records (38 + 19 of 64 interleaved channels per 256-B record), so those lines come from HBM
 // once, into that XCD's L2, instead of once per XCD.  n_frames: frames of the launch; tx, ty:
-// tiles per plane.
+// tiles per plane.  Only for launches of >= 8 frames (xcd_major): with fewer, every tile of a frame
+// would run on one XCD (one frame: 32 of 256 CUs, 7/8 of the grid exiting at once), so small
+// launches take the plain order, which spreads a frame's tiles over the whole chip (advisor r04).
 template <class Src, int R>
 __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const double* __restrict__ w, int rr,
                                                   float thresh, int cap, int32_t* __restrict__ stage_key,
                                                   float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt,
-                                                  int n_frames, int tx, int ty) {
+                                                  int n_frames, int tx, int ty, int xcd_major) {
   constexpr int kTP = kFU + 2;  // vertical-pass output pitch (16-byte aligned rows)
   constexpr int kHP = kFT + 4;  // filtered-map pitch
   constexpr int NB = 4;         // outputs per thread in the register-blocked passes
@@ -803,10 +805,17 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
   __shared__ int wlo[2], whi[2];
   const int r = R > 0 ? R : rr;
   const int per_frame = tx * ty * OP_N_JOINTS;
-  const int lin = blockIdx.x, xcd = lin & 7, slot = lin >> 3;
-  const int f = (slot / per_frame) * 8 + xcd;
+  const int lin = blockIdx.x;
+  int f, within;
+  if (xcd_major) {
+    const int xcd = lin & 7, slot = lin >> 3;
+    f = (slot / per_frame) * 8 + xcd;
+    within = slot - (slot / per_frame) * per_frame;
+  } else {  // plain order: a frame's tiles spread over every XCD
+    f = lin / per_frame;
+    within = lin - f * per_frame;
+  }
   if (f >= n_frames) return;
-  const int within = slot - (slot / per_frame) * per_frame;
   const int j = within / (tx * ty), t = within - j * (tx * ty);
   const int fj = f * OP_N_JOINTS + j;
   const int x0 = (t % tx) * kFT, y0 = (t / tx) * kFT;
@@ -1056,13 +1065,14 @@ static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hi
                      also, also ? also_n : 0);
   OP_AFTER_LAUNCH("zero_counters", st);
   const int tx = (s.mw + kFT - 1) / kFT, ty = (s.mh + kFT - 1) / kFT;
-  const dim3 g((unsigned)(8 * ((s.n + 7) / 8) * tx * ty * OP_N_JOINTS));
+  const int xm = s.n >= 8;
+  const dim3 g((unsigned)((xm ? 8 * ((s.n + 7) / 8) : s.n) * tx * ty * OP_N_JOINTS));
   if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
     hipLaunchKernelGGL((heat_fused<Src, 10>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
-                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty);
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty, xm);
   else
     hipLaunchKernelGGL((heat_fused<Src, 0>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
-                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty);
+                       s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty, xm);
   OP_AFTER_LAUNCH("heat_fused<Src>", st);
   if (b.maxp <= 2048) {
     hipLaunchKernelGGL(peak_sort, dim3((unsigned)planes), dim3(512), 0, st, b.stage_key, b.stage_score, b.maxp, s.mw,

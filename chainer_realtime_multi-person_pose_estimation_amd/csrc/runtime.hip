@@ -231,8 +231,12 @@ struct PostRecord {
 // holds), copied aside on the device when the records are packed, so the owning rank can re-run
 // them after the next step has overwritten the batched buffers (op_comm_overflow*).
 struct KeepSlot {
-  // kept frames are compacted into `slots` entries (OP_KEEP_FRAMES, default 8; advisor r03: sizing
-  // these for every frame of the pack cost GBs per slot at 1280x720), assigned by device counters
+  // kept frames are compacted into `slots` entries assigned by device counters.  Round 5 (advisor
+  // r04): every frame of the pack gets a slot while their maps fit kKeepSlotBytes (the 368x368 maps
+  // of 232 frames: 125 MB; 16 precise 1280x720 frames: 3.4 GB), at least 8 beyond that, and a
+  // gather that had more overflow frames than slots grows the next packs' slots (`grow`);
+  // OP_KEEP_FRAMES=<n> pins the count (test aid).  A frame left without a slot is reported as a
+  // frame status through the overflow exchange (frames.py), never as an exception before it
   float* maps = nullptr;  // [slot][fstride] post-process input of frames over the batched caps
   size_t maps_cap = 0;  // bytes
   double* res = nullptr;  // [slot][maxs][54 + 1] rows of frames past max_persons not in h_rows
@@ -258,8 +262,10 @@ struct KeepSlot {
   int32_t* d_rows_cnt = nullptr;  // [0] h_rows allocator, [1] maps slots, [2] res slots
   PostRecord rec{};
   int n = 0;
+  int grow = 0;  // overflow frames of the largest gather seen that needed a slot
 };
 constexpr int kKeepHdr = 5;  // int32 per frame in KeepSlot::d_hdr / h_hdr
+constexpr int64_t kKeepSlotBytes = 4ll << 30;  // keep-slot map bytes per gather slot (of 288 GB HBM)
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
@@ -2441,7 +2447,15 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     const float* src = r.kind == 1 ? r.low.base : r.kind == 2 ? r.full : nullptr;
     const int64_t fstride = r.kind == 1 ? r.low.fstride : r.fstride;
     const char* kf_env = getenv("OP_KEEP_FRAMES");
-    k.slots = std::min(n, kf_env ? std::max(1, atoi(kf_env)) : 8);
+    if (kf_env) {
+      k.slots = std::min(n, std::max(1, atoi(kf_env)));
+    } else {
+      const char* kb_env = getenv("OP_KEEP_BYTES");  // test aid: the map-byte budget per gather slot
+      const int64_t budget = kb_env ? std::max(0ll, atoll(kb_env)) : kKeepSlotBytes;
+      const int64_t per = src ? std::max<int64_t>(1, fstride * 4) : 1;
+      const int64_t fit = std::max<int64_t>(8, budget / per);
+      k.slots = (int)std::min<int64_t>(n, std::max<int64_t>(fit, std::max(c->keep[0].grow, c->keep[1].grow)));
+    }
     if (src) {
       RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)k.slots * fstride * 4, "keep_maps"));
       RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)k.slots * OP_N_JOINTS * 4, "keep_cnt"));
@@ -2486,16 +2500,19 @@ int ctx_kept_overflow(op_ctx* c, int slot, int32_t* frames, int32_t* reasons, in
     set_error("kept overflow: bad arguments");
     return OP_ERR_INVALID;
   }
-  const KeepSlot& k = c->keep[slot];
-  int m = 0;
+  KeepSlot& k = c->keep[slot];
+  int m = 0, need1 = 0, need2 = 0;
   for (int i = 0; i < k.n; ++i)
     if (k.h_hdr[kKeepHdr * i + 3]) {
+      if (k.h_hdr[kKeepHdr * i + 3] == 1) ++need1;
+      else if (k.h_hdr[kKeepHdr * i + 4] < 0) ++need2;  // rows past the page-locked buffer
       if (m < cap) {
         frames[m] = i;
         if (reasons) reasons[m] = k.h_hdr[kKeepHdr * i + 3];
       }
       ++m;
     }
+  k.grow = std::max(k.grow, std::max(need1, need2));  // the next packs keep this many
   *count = m;
   return OP_OK;
 }

@@ -88,6 +88,16 @@ def unpack_full(buf):
     return unpack_records(bytes(buf[8:]), mp) if n else []
 
 
+def exchange_overflow(transport, own):
+    """The per-step overflow exchange (collective over the TCP transport): every rank's whole results
+    of its frames that the records could not carry -- including frames no keep slot held, as status
+    OP_ERR_CAPACITY -- to rank 0 (other ranks: None)."""
+    if transport.world == 1:
+        return own
+    got = transport.gather(pack_full(own))
+    return None if got is None else [r for g in got for r in unpack_full(g)]
+
+
 def merge_overflow(records, overflow):
     """Records (unpacked) with the whole results of the overflow frames in place of theirs."""
     if not overflow:
@@ -111,6 +121,7 @@ def count_persons(buf, max_persons, overflow=()):
         r = ovf.get(int(fid[i]))
         if r is not None:
             persons += len(r[4]) if r[1] == 0 else 0
+            missing += r[1] == STATUS_CAPACITY  # no keep slot held it (RcclGather._own_overflow)
         elif hdr[i, 0] == 0:
             persons += int(hdr[i, 2])
         elif hdr[i, 0] == STATUS_CAPACITY:
@@ -289,6 +300,8 @@ class RcclGather(object):
         self._sub = []  # (frame_base, frame_stride) of the outstanding submits, oldest first
         self.overflow_s = 0.0  # host time spent on this rank's overflow frames (re-runs, row copies)
         self.overflow_caps = 0  # of them, frames over the batched caps (re-run uncapped)
+        self.lost = 0  # of them, frames no keep slot held: status OP_ERR_CAPACITY in their result
+        self.lost_msg = ""
 
     def submit(self, first, n, frame_base, frame_stride):
         """Enqueue the gather of this rank's staged frames [first, first+n) (global ids
@@ -323,6 +336,15 @@ class RcclGather(object):
                     cap = res.n_persons
                     continue
                 break
+            if rc == lib_.OP_ERR_CAPACITY:
+                # no keep slot held this frame (more overflow frames than slots in one gather; the
+                # library grows the slots for the next packs): it travels as a frame status through
+                # the exchange below -- an exception here would leave the other ranks waiting in it
+                self.lost += 1
+                self.lost_msg = lib_.last_error()
+                out.append((base + int(i) * stride, STATUS_CAPACITY, int(res.n_peaks),
+                            np.empty((0, N_JOINTS, 3)), np.empty(0)))
+                continue
             if rc != lib_.OP_OK and rc != res.status:  # a frame status (e.g. the reference's IndexError) travels
                 lib_.check(rc, "op_comm_overflow_result")
             k = res.n_persons if res.status == 0 else 0
@@ -343,11 +365,7 @@ class RcclGather(object):
         t0 = time.perf_counter()
         own = self._own_overflow(base, stride)
         self.overflow_s += time.perf_counter() - t0
-        if self.t.world > 1:
-            got = self.t.gather(pack_full(own))
-            ovf = None if got is None else [r for g in got for r in unpack_full(g)]
-        else:
-            ovf = own
+        ovf = exchange_overflow(self.t, own)
         if not p.value:
             return None
         buf = ct.string_at(p.value, nf.value * rb.value)

@@ -76,6 +76,12 @@ typedef struct op_frame_result {
 typedef struct op_ctx op_ctx;
 
 const char* op_last_error(void);
+
+/* Provenance of the loaded binary (no reference counterpart): writes "sha256:<64 hex>" + NUL into
+ * out (cap >= 72), the digest of the library's sources as built -- sha256 of the `sha256sum`
+ * listing of csrc/ *.hip *.hpp *.cpp, csrc/Makefile and include/ *.h (paths relative to csrc/, sorted),
+ * computed by the Makefile at build time; _lib.source_digest() recomputes it from the tree. */
+int op_build_info(char* out, int32_t cap);
 int op_default_params(op_params* p);
 int op_default_limits(op_limits* l);
 
@@ -297,7 +303,7 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_7X7_TIGHT 24   /* conv_m16 7x7 launches with the tight halo pitch w + 6 (wide maps) */
 #define OP_CENSUS_CUBIC_FUSED 25 /* detect_precise map resizes as one fused pass (resize_cubic_fused_mean) */
 #define OP_CENSUS_CUBIC_TWO_PASS 26 /* ... as the two-pass path (padded-size maps in HBM) */
-#define OP_CENSUS_SPLITK_INKERNEL 27 /* split-K launches (7x7 or 3x3) finished by their last split, no reduce launch */
+/* slot 27: retired in round 5 (the in-kernel split-K experiment was removed) */
 #define OP_CENSUS_CUBIC_ROWS 28  /* two-pass second resize as one row-block launch for the batch
                                     (resize_cubic_f32_planar_mean_rows), else one launch per frame */
 #define OP_CENSUS_SLOTS 32

@@ -22,6 +22,17 @@ def test_header_symbols_exported(lib):
     assert sorted(lib.EXPORTED) == decl
 
 
+def test_loaded_library_is_built_from_this_tree(lib):
+    """op_build_info reports the digest of the sources the loaded .so was
+    compiled from (csrc/Makefile bakes it in); it must equal the digest of the checked-out csrc/ and
+    include/ -- a stale or foreign binary fails here (and in smoke() on the GPU box)."""
+    got = lib.build_info()
+    assert re.fullmatch(r"sha256:[0-9a-f]{64}", got), got
+    assert got == lib.source_digest(), "libopenpose_hip.so was not built from this tree's sources: rebuild it"
+    buf = ctypes.create_string_buffer(8)
+    assert lib.lib().op_build_info(buf, len(buf)) == lib.OP_ERR_INVALID  # too small: refused, nothing written
+
+
 def test_layer_table_matches_cocoposenet(lib):
     from oracle.forward import LAYERS
     assert lib.layer_table() == LAYERS

@@ -196,3 +196,47 @@ def test_bench_gather_transport_is_one_for_all_ranks():
     for p in ps:
         p.join(timeout=30)
     assert got == [(0, "HostGather", False, True, True), (1, "HostGather", False, False, True)], got
+
+
+def _lost_worker(rank, world, port, q):
+    """One step of RcclGather.wait's host side on each rank: records of this rank's frames (rank 1's first
+    frame is one that no keep slot held), then the overflow
+    exchange -- the lost frame travels as a status, no rank raises before the collective."""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from importlib import import_module
+    F = import_module("chainer_realtime_multi-person_pose_estimation_amd.frames")
+    t = F.SocketTransport(rank, world, port=port, timeout=60)
+    ids = [i for i in F.shard(6, rank, world)]
+    res = _frame_results(ids)
+    own = []
+    if rank == 1:
+        fid, _, npk, _, _ = res[0]
+        own = [(fid, F.STATUS_CAPACITY, npk, np.empty((0, 18, 3)), np.empty(0))]
+    recs = F.pack_records(res, MAXP)
+    got = t.gather(recs.tobytes())
+    ovf = F.exchange_overflow(t, own)
+    t.barrier()  # every rank got past the exchange
+    if rank == 0:
+        raw = b"".join(got)
+        q.put((F.count_persons(raw, MAXP, ovf), [(r[0], r[1]) for r in ovf]))
+    t.close()
+
+
+def test_lost_keep_slot_frame_travels_as_status():
+    """Advisor r04 (medium): a frame that no keep slot held is reported through the overflow exchange
+    as status OP_ERR_CAPACITY (counted as not delivered), instead of an exception on its rank before
+    the exchange that would leave the other ranks blocked in it."""
+    F = pkg_module("frames")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lost_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    (persons, missing), ovf = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert missing == 1 and len(ovf) == 1 and ovf[0][1] == F.STATUS_CAPACITY
+    assert persons > 0

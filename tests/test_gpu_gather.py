@@ -166,10 +166,11 @@ def test_every_frame_reaches_rank0_whole(ctx, rows_avg, monkeypatch):
 
 
 def test_keep_slots_are_bounded(ctx, monkeypatch):
-    """Advisor r03 (low): the keep buffers hold OP_KEEP_FRAMES (default 8) compacted frames, not every
-    frame of the pack.  With OP_KEEP_ROWS_AVG=0 every frame past max_persons goes through a device
-    keep slot; with OP_KEEP_FRAMES=1 the second such frame of one gather has no slot, and collecting
-    the step fails loudly (OP_ERR_CAPACITY) instead of returning another frame's rows."""
+    """Keep slots (advisor r03 low, r04 medium).  With OP_KEEP_ROWS_AVG=0 every frame past max_persons
+    goes through a device keep slot.  OP_KEEP_FRAMES=1 pins one slot: the second such frame of the
+    gather has none, and it reaches the caller as a frame status (OP_ERR_CAPACITY, counted as not
+    delivered) through the overflow exchange -- no exception before that collective, which would
+    leave the other ranks waiting in it; never another frame's rows."""
     monkeypatch.setenv("OP_KEEP_ROWS_AVG", "0")
     monkeypatch.setenv("OP_KEEP_FRAMES", "1")
     F = pkg_module("frames")
@@ -183,14 +184,59 @@ def test_keep_slots_are_bounded(ctx, monkeypatch):
         ctx.use_staged_maps(True)
         ctx.run_staged()
         g.submit(0, n, 0, 1)
-        with pytest.raises(RuntimeError, match="keep slots"):
-            g.wait(raw=True)
+        raw, ovf = g.wait(raw=True)
+        assert g.lost == 1 and "keep slots" in g.lost_msg, (g.lost, g.lost_msg)
+        st = sorted((r[0], r[1]) for r in ovf)
+        assert st[0][1] == 0 and st[1][1] == F.STATUS_CAPACITY, st  # one kept whole, one reported lost
+        assert F.count_persons(raw, MAXP, ovf)[1] == 1
         monkeypatch.setenv("OP_KEEP_FRAMES", "2")  # read per pack: both frames kept again
         ctx.run_staged()
         g.submit(0, n, 0, 1)
         raw, ovf = g.wait(raw=True)
-        assert sorted(r[0] for r in ovf) == [0, 1]
+        assert sorted(r[0] for r in ovf) == [0, 1] and all(r[1] == 0 for r in ovf)
         assert F.count_persons(raw, MAXP, ovf)[1] == 0
     finally:
         ctx.use_staged_maps(False)
+        g.close()
+
+
+@pytest.fixture
+def fresh_ctx(lib, rand_weights):
+    c = lib.Context(0)  # keep-slot growth is per context: start from none
+    c.set_weights(rand_weights)
+    yield c
+    c.close()
+
+
+def test_keep_slots_grow_after_a_short_gather(fresh_ctx, monkeypatch):
+    """Default sizing: every frame of the pack gets a slot while their maps fit the byte budget, at
+    least 8 beyond it; a gather with more overflow frames than slots makes the next packs keep that
+    many.  With a budget of 1 byte (OP_KEEP_BYTES, test aid) 10 frames past max_persons get 8 slots:
+    two are reported lost, and the next gather keeps all ten whole."""
+    monkeypatch.setenv("OP_KEEP_ROWS_AVG", "0")
+    monkeypatch.setenv("OP_KEEP_BYTES", "1")
+    monkeypatch.delenv("OP_KEEP_FRAMES", raising=False)
+    F = pkg_module("frames")
+    six = load_golden("six_people")
+    six_maps = np.concatenate([six["paf_low"], six["heat_low"]])
+    n = 10
+    fresh_ctx.stage_frames(np.zeros((n, 368, 368, 3), np.uint8))
+    g = F.RcclGather(fresh_ctx, F.SocketTransport(0, 1), max_persons=MAXP, timeout=60)
+    try:
+        fresh_ctx.stage_maps(np.stack([six_maps] * n))
+        fresh_ctx.use_staged_maps(True)
+        fresh_ctx.run_staged()
+        g.submit(0, n, 0, 1)
+        raw, ovf = g.wait(raw=True)
+        assert g.lost == 2 and F.count_persons(raw, MAXP, ovf)[1] == 2
+        fresh_ctx.run_staged()
+        g.submit(0, n, 0, 1)
+        raw, ovf = g.wait(raw=True)
+        assert g.lost == 2 and len(ovf) == n and all(r[1] == 0 for r in ovf)
+        assert F.count_persons(raw, MAXP, ovf)[1] == 0
+        want = fresh_ctx.fetch_results(0, n)
+        for r in ovf:
+            assert np.array_equal(r[3], np.asarray(want[r[0]][0]).reshape(r[3].shape)), r[0]
+    finally:
+        fresh_ctx.use_staged_maps(False)
         g.close()

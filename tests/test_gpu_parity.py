@@ -179,44 +179,6 @@ def test_forward_7x7_tile_sizes_agree(ctx):
         assert err <= 1e-4 * mag, (i, err, mag)  # 10x inside the 1e-3 parity tolerance
 
 
-def test_splitk_in_kernel_equals_reduce_launch(ctx, lib, monkeypatch):
-    """Round 4 experiment (opt-in OP_SPLITK_INKERNEL=1, measured slower): a split-K launch (one
-    frame's 7x7 and 3x3 layers) finishes in the conv kernel -- the last split of each tile to arrive
-    (sc1 partials, agent-scope counter) sums the partials in split order (conv_big.hpp splitk_arrive
-    / splitk_reduce_item) -- instead of in a conv_m16_splitk_reduce launch.  Same arithmetic in the
-    same order: maps BIT-IDENTICAL to the default, eager and under hipGraph replay (the counters are
-    reset by their last arrivals)."""
-    rng = np.random.default_rng(27)
-    x = rng.uniform(-0.5, 0.5, (1, 3, 368, 368)).astype(np.float32)
-    monkeypatch.setenv("OP_SPLITK_INKERNEL", "1")
-    lib.conv_census(reset=True)
-    fused = ctx.forward(x)
-    cen = lib.conv_census(reset=True)
-    assert cen["splitk_inkernel"] > 0 and cen["7x7_splitk"] > 0 and cen["3x3_splitk"] > 0, cen
-    again = ctx.forward(x)  # counters back at zero after every launch
-    lib.conv_census(reset=True)
-    monkeypatch.setenv("OP_SPLITK_INKERNEL", "0")
-    plain = ctx.forward(x)
-    cen = lib.conv_census(reset=True)
-    monkeypatch.delenv("OP_SPLITK_INKERNEL")
-    assert cen["splitk_inkernel"] == 0 and cen["7x7_splitk"] > 0, cen
-    for a, b, c in zip(fused, again, plain):
-        assert np.array_equal(a, b) and np.array_equal(a, c), float(np.abs(a - c).max())
-    # staged frames through the captured graph (in-kernel path) vs eager with reduce launches
-    frames = rng.integers(0, 256, (1, 368, 368, 3), dtype=np.uint8)
-    monkeypatch.setenv("OP_SPLITK_INKERNEL", "0")
-    want = ctx.detect(frames[0])
-    monkeypatch.setenv("OP_SPLITK_INKERNEL", "1")
-    ctx.stage_frames(frames)
-    for graph in (False, True, True):
-        ctx.run_staged(graph=graph)
-        ctx.synchronize()
-        p, s, r = ctx.fetch_result(0)
-        assert r.n_peaks == want[2].n_peaks
-        assert np.array_equal(p, want[0]) and np.array_equal(s, want[1])
-    monkeypatch.delenv("OP_SPLITK_INKERNEL")
-
-
 def test_forward_precisions_agree(ctx, rand_weights):
     """bf16x3 vs exact-f32 MFMA on a 720p-shaped input (656x368), batch 2."""
     rng = np.random.default_rng(2)
