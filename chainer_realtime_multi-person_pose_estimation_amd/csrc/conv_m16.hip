@@ -2,6 +2,10 @@
 // shared halo / weight-ring scheme).  Own translation unit: built with the Makefile's FLAGS_conv_m16.
 #include "conv_big.hpp"
 
+#ifndef M16_DMA_HALF
+#define M16_DMA_HALF 0
+#endif
+
 namespace op {
 
 // ---- 7x7 on v_mfma_f32_16x16x32_bf16, raster tiles (the default 7x7 kernel) ----
@@ -74,6 +78,10 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int64_t wstep = 4 * wplane;
   const char* const wsrc = (const char*)g.w + (wave / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
   const int wdst = (wave / 2) * PLANE_W + (wave % 2) * 1024;
+#if M16_DMA_HALF  // experiment: waves 0-3 (one per SIMD) copy pieces w and w + 4, waves 4-7 only compute
+  const char* const wsrc4 = (const char*)g.w + ((wave + 4) / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
+  const int wdst4 = ((wave + 4) / 2) * PLANE_W + (wave % 2) * 1024;
+#endif
   // split-K (tl.ksplit > 1): this workgroup runs input chunks [cb0, cb1)
   const int nsplit = tl.ksplit > 1 ? tl.ksplit : 1;
   const int split = nsplit > 1 ? (int)blockIdx.y : 0;
@@ -82,13 +90,21 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   // a padding tap whose weights are staged from device zeros, so every pair is a full K = 32 step
   // (no per-pair masking of the A fragments)
   constexpr int KSQP = KSQ + (KSQ & 1);
+  constexpr int kDmaPerPair = M16_DMA_HALF ? 4 : 2;  // weight pieces a (staging) wave issues per tap pair
   const int n_it = cb1 * KSQP;
   const char* const zsrc = (const char*)tl.zeros + lane * 16;
   auto stage_w = [&](int it) {
     char* dst = ring + ((unsigned)it % RING) * SLOT_W;
     if (it >= n_it) it = n_it - 1;
     const int c = it / KSQP, tp = it - c * KSQP;
+#if M16_DMA_HALF
+    if (wave < 4) {
+      glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
+      glds16(tp < KSQ ? (const void*)(wsrc4 + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst4);
+    }
+#else
     glds16(tp < KSQ ? (const void*)(wsrc + (int64_t)(c * KSQ + tp) * wstep) : (const void*)zsrc, dst + wdst);
+#endif
   };
 
   // the tile's geometry: pixels [P0, P1] of the batch, frame / first row, the second frame's rows
@@ -145,6 +161,9 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
 
   const Tile T = tile_of(widx);
+#if M16_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
   for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
   {
@@ -189,13 +208,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #endif
 #pragma unroll 1
       for (int t = 0; t < kPairsEnd; t += 2, it += 2) {
-        wait_vmcnt<2 * AHEAD - 2>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
+        wait_vmcnt<kDmaPerPair * (AHEAD - 1)>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
 #if !M16_PROBE_NOBAR  // timing probe only (racy ring): no per-pair barrier
         __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
 #endif
         asm volatile("" ::: "memory");
+#if !defined(M16_STAGE_MID)
         stage_w(it + 2 * AHEAD);
         stage_w(it + 2 * AHEAD + 1);
+#endif
         // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
         // tap (zero weights) reads tap t's pixels: finite values, times zero
         const int t1 = t + 1 < KSQ ? t + 1 : t;
@@ -226,6 +247,14 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
           }
+#if defined(M16_STAGE_MID)  // experiment: the next pairs' weight DMA issued after block M16_STAGE_MID's MFMAs
+          if (pb == (M16_STAGE_MID < NPX ? M16_STAGE_MID : NPX - 1)) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_w(it + 2 * AHEAD);
+            stage_w(it + 2 * AHEAD + 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#endif
         }
       }
     }

@@ -217,6 +217,7 @@ def test_one_frame_pooled_split_k(lib, rand_weights):
         assert np.array_equal(graph[0], eager[0]) and np.array_equal(graph[1], eager[1])
         c.set_batch_invariant(True)
         try:
+            lib.conv_census(reset=True)  # (the graph captures above counted their launches)
             c.run_staged()
             c.synchronize()
             cen_i = lib.conv_census(reset=True)

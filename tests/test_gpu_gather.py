@@ -186,8 +186,8 @@ def test_keep_slots_are_bounded(ctx, monkeypatch):
         g.submit(0, n, 0, 1)
         raw, ovf = g.wait(raw=True)
         assert g.lost == 1 and "keep slots" in g.lost_msg, (g.lost, g.lost_msg)
-        st = sorted((r[0], r[1]) for r in ovf)
-        assert st[0][1] == 0 and st[1][1] == F.STATUS_CAPACITY, st  # one kept whole, one reported lost
+        # the slot goes to whichever frame's block claims it first: one kept whole, one reported lost
+        assert sorted(r[1] for r in ovf) == [0, F.STATUS_CAPACITY] and sorted(r[0] for r in ovf) == [0, 1], ovf
         assert F.count_persons(raw, MAXP, ovf)[1] == 1
         monkeypatch.setenv("OP_KEEP_FRAMES", "2")  # read per pack: both frames kept again
         ctx.run_staged()

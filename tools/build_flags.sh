@@ -7,7 +7,7 @@ NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=chainer_realtime_multi-person_pose_estimation_amd
 W=/tmp/opflags_$NAME; rm -rf $W; mkdir -p $W/$PKG/csrc $W/include
-cp $ROOT/$PKG/csrc/*.hip $ROOT/$PKG/csrc/*.hpp $ROOT/$PKG/csrc/Makefile $W/$PKG/csrc/
+cp $ROOT/$PKG/csrc/*.hip $ROOT/$PKG/csrc/*.hpp $ROOT/$PKG/csrc/*.cpp $ROOT/$PKG/csrc/Makefile $W/$PKG/csrc/
 cp $ROOT/include/*.h $W/include/
 make -s -j8 -C $W/$PKG/csrc "$@"
 cp $W/$PKG/libopenpose_hip.so $ROOT/$PKG/libopenpose_hip.$NAME.so
