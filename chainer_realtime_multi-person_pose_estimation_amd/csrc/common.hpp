@@ -92,6 +92,8 @@ struct ConvShape {
 };
 
 int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st);
+// conv_f32.hip: the 3x3 / 7x7 LDS-halo form of conv_mfma_f32 (bit-identical); *taken = 0 outside it
+int launch_conv_f32_lds(const ConvShape& s, const ConvGroup* g, hipStream_t st, int* taken);
 
 // a branch's two closing 1x1 convs fused, exact f32 (conv.hip conv_head_f32)
 struct HeadF32Shape {

@@ -154,6 +154,9 @@ int launch_conv(const ConvShape& s, const ConvGroup* g, hipStream_t st) {
       return OP_ERR_INVALID;
     }
   }
+  int taken = 0;
+  const int rc = launch_conv_f32_lds(s, g, st, &taken);  // 3x3 / 7x7: the LDS-halo form (conv_f32.hip)
+  if (rc != OP_OK || taken) return rc;
   switch (s.ks) {
     case 1: return launch_conv_t<1, 2, 2>(s, g, st);
     case 3: return launch_conv_t<3, 2, 2>(s, g, st);

@@ -2,11 +2,28 @@
 // shared halo / weight-ring scheme).  Own translation unit: built with the Makefile's FLAGS_conv_m16.
 #include "conv_big.hpp"
 
+// Round 5: the weight ring is staged by waves 0-3 only (one wave per SIMD, 4 pieces per tap pair),
+// so on every SIMD one wave issues the LDS-DMA while its partner keeps issuing MFMAs; with all 8
+// waves staging 2 pieces each, both waves of a SIMD paused for the DMA issue after the same ring
+// barrier.  7x7 class -0.6..-1.1 % in 6 interleaved rounds on two boxes
+// (profiles/r05/ab_r05c_7x7_dma_placement.log, ab_r05d_dmahalf.log); -DM16_DMA_HALF=0 restores it.
 #ifndef M16_DMA_HALF
-#define M16_DMA_HALF 0
+#define M16_DMA_HALF 1
 #endif
 
 namespace op {
+
+#if M16_STAMPS
+// Diagnostic build only (tools/build_variant.sh ... -DM16_STAMPS=1; never the product library):
+// per-wave s_memtime sums over each 7x7 launch, added into these counters by vector atomics and
+// read back by launch_m16_7x7 (OP_M16_STAMPS=1): [0] whole wave, [1] chunk boundaries (halo
+// reload: two barriers + DMA wait), [2] pair starts (vmcnt wait, ring barrier, DMA issue, A / B
+// fragment reads up to the first MFMA's issue), [3] pair loops incl. boundaries, [4] epilogue,
+// [5] pairs, [6] waves, [7] after the pair loop before the epilogue (final vmcnt wait); pair start
+// split: [8] the ring vmcnt wait, [9] the ring barrier, [10] the weight DMA issue
+__device__ unsigned long long g_m16_st[12];
+#define M16_T() __builtin_amdgcn_s_memtime()
+#endif
 
 // ---- 7x7 on v_mfma_f32_16x16x32_bf16, raster tiles (the default 7x7 kernel) ----
 // K = 32 of the 16x16x32 form is fed with a tap PAIR of one 16-channel chunk: lane group
@@ -78,7 +95,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int64_t wstep = 4 * wplane;
   const char* const wsrc = (const char*)g.w + (wave / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
   const int wdst = (wave / 2) * PLANE_W + (wave % 2) * 1024;
-#if M16_DMA_HALF  // experiment: waves 0-3 (one per SIMD) copy pieces w and w + 4, waves 4-7 only compute
+#if M16_DMA_HALF  // waves 0-3 (one per SIMD) copy pieces w and w + 4, waves 4-7 only compute
   const char* const wsrc4 = (const char*)g.w + ((wave + 4) / 2) * wplane + ((int64_t)co0 + 64 * (wave % 2) + lane) * 16;
   const int wdst4 = ((wave + 4) / 2) * PLANE_W + (wave % 2) * 1024;
 #endif
@@ -160,10 +177,10 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   };
   const int wlane = (2 * khalf) * PLANE_W + (ch * 64 + l16) * 16;     // A: channel ch*64 + cb*16 + l16
 
-  const Tile T = tile_of(widx);
-#if M16_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#if M16_STAMPS
+  const unsigned long long st_t0 = M16_T();
 #endif
+  const Tile T = tile_of(widx);
 #pragma unroll
   for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
   {
@@ -189,7 +206,16 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       for (int pb = 0; pb < NPX; ++pb) acc[cb][pb] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     int it = cb0 * KSQP;
+#if M16_STAMPS
+    unsigned long long st_b = 0, st_p = 0, st_np = 0, st_v = 0, st_bar = 0, st_dma = 0;
+    const unsigned long long st_loop0 = M16_T();
+#endif
     for (int c = cb0; c < cb1; ++c) {
+#if M16_STAMPS
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tb0 = M16_T();
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
 #if M16_PROBE_NOHALO  // timing probe only (wrong results): the halo is loaded for the first chunk only
@@ -200,6 +226,11 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#if M16_STAMPS
+      __builtin_amdgcn_sched_barrier(0);
+      st_b += M16_T() - tb0;
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       bf16x8g ah[4], al[4];
 #if M16_PROBE_NOPAD  // timing probe only (wrong results): the padding pair of the odd 49th tap skipped
       constexpr int kPairsEnd = KSQ - 1;
@@ -208,14 +239,36 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #endif
 #pragma unroll 1
       for (int t = 0; t < kPairsEnd; t += 2, it += 2) {
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tp0 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+        ++st_np;
+#endif
         wait_vmcnt<kDmaPerPair * (AHEAD - 1)>();  // W(it), W(it+1) (issued AHEAD pairs back) ...
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tp1 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #if !M16_PROBE_NOBAR  // timing probe only (racy ring): no per-pair barrier
         __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
 #endif
         asm volatile("" ::: "memory");
-#if !defined(M16_STAGE_MID)
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tp2 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         stage_w(it + 2 * AHEAD);
         stage_w(it + 2 * AHEAD + 1);
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tp3 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+        st_v += tp1 - tp0;
+        st_bar += tp2 - tp1;
+        st_dma += tp3 - tp2;
 #endif
         // tap offsets of the pair (uniform: scalar), then one select per lane (tsel); the padding
         // tap (zero weights) reads tap t's pixels: finite values, times zero
@@ -244,21 +297,30 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+#if M16_STAMPS
+            if (pb == 0 && cb == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+              st_p += M16_T() - tp0;
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
           }
-#if defined(M16_STAGE_MID)  // experiment: the next pairs' weight DMA issued after block M16_STAGE_MID's MFMAs
-          if (pb == (M16_STAGE_MID < NPX ? M16_STAGE_MID : NPX - 1)) {
-            __builtin_amdgcn_sched_barrier(0);
-            stage_w(it + 2 * AHEAD);
-            stage_w(it + 2 * AHEAD + 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-#endif
         }
       }
     }
+#if M16_STAMPS
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long st_loop1 = M16_T();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     wait_vmcnt<0>();
+#if M16_STAMPS
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long st_wait1 = M16_T();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 
     if (nsplit > 1) {  // raw partial sums; conv_m16_splitk_reduce adds the splits, bias and ReLU
       const int wsc = max(g0.cop, g1.cop);  // partial row stride (the launcher sizes ws with it)
@@ -299,6 +361,24 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         }
       }
     }
+#if M16_STAMPS
+    wait_vmcnt<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long st_end = M16_T();
+    if (lane == 0) {
+      atomicAdd(&g_m16_st[0], st_end - st_t0);
+      atomicAdd(&g_m16_st[1], st_b);
+      atomicAdd(&g_m16_st[2], st_p);
+      atomicAdd(&g_m16_st[3], st_loop1 - st_loop0);
+      atomicAdd(&g_m16_st[4], st_end - st_wait1);
+      atomicAdd(&g_m16_st[5], st_np);
+      atomicAdd(&g_m16_st[6], 1ull);
+      atomicAdd(&g_m16_st[7], st_wait1 - st_loop1);
+      atomicAdd(&g_m16_st[8], st_v);
+      atomicAdd(&g_m16_st[9], st_bar);
+      atomicAdd(&g_m16_st[10], st_dma);
+    }
+#endif
   }
 }
 
@@ -321,6 +401,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
     set_error("conv_m16_bf16x3: halo plane over 32 KiB");
     return OP_ERR_INVALID;
   }
+
   // small tiles whose halo planes fit 16 KiB take the deep weight ring (12 taps, 5 pairs ahead)
   static const bool no_deep = getenv("OP_M16_NODEEP") && atoi(getenv("OP_M16_NODEEP")) != 0;  // A/B aid
   const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
@@ -352,6 +433,30 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
       break;
     default: hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g0, g1, tl);
   }
+#if M16_STAMPS
+  static const bool dump = getenv("OP_M16_STAMPS") != nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (dump && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone && tl.ksplit == 1) {
+    static unsigned long long tot[12] = {};
+    static int launches = 0;
+    unsigned long long h[12];
+    OP_HIP_CHECK(hipStreamSynchronize(st));
+    OP_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_m16_st), sizeof(h)));
+    const unsigned long long z[12] = {};
+    OP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_m16_st), z, sizeof(z)));
+    for (int i = 0; i < 12; ++i) tot[i] += h[i];
+    if (++launches % 25 == 0) {
+      const double w = (double)tot[0];
+      fprintf(stderr,
+              "M16_STAMPS npx %d launches %d waves %llu pairs/wave %.1f | per wave cycles %.0f | chunk boundary %.4f "
+              "pair start %.4f (vmcnt %.4f barrier %.4f dma %.4f) pair loop %.4f (pure pairs %.4f) final wait %.4f "
+              "epilogue %.4f prologue %.4f\n",
+              npx, launches, tot[6], (double)tot[5] / tot[6], w / tot[6], tot[1] / w, tot[2] / w, tot[8] / w, tot[9] / w,
+              tot[10] / w, tot[3] / w,
+              (tot[3] - tot[1] - tot[2]) / w, tot[7] / w, tot[4] / w, (w - tot[3] - tot[7] - tot[4]) / w);
+    }
+  }
+#endif
   return OP_OK;
 }
 
