@@ -46,14 +46,14 @@ struct F32Tile {
   static constexpr int LDS = 2 * BUF;           // double-buffered
 };
 
-template <int KS, int TCW>
-__global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, ConvGroup g1, int tiles_x, int tiles_y) {
+template <int KS, int TCW, int CB = 2>
+__global__ __launch_bounds__(256, CB == 4 ? 2 : 1) void conv_f32_lds(ConvShape s, ConvGroup g0, ConvGroup g1, int tiles_x, int tiles_y) {
   using T = F32Tile<KS, TCW>;
   constexpr int KSQ = KS * KS;
   constexpr int R = T::R;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const ConvGroup g = blockIdx.z == 0 ? g0 : g1;
-  const int co_base = blockIdx.y * 64;
+  const int co_base = blockIdx.y * (CB * 32);
   if (co_base >= g.cop) return;
   const int tpf = tiles_x * tiles_y;
   const int frame = blockIdx.x / tpf;
@@ -95,19 +95,19 @@ __global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, C
   const int64_t wstep = (int64_t)g.cop * 8;
   const int n_it = s.c8 * KSQ;
 
-  floatx16 acc[2][2];
+  floatx16 acc[CB][2];
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
+  for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
     for (int pb = 0; pb < 2; ++pb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[cb][pb][r] = 0.0f;
 
-  auto load_a = [&](floatx4(&a)[2], int it) {
+  auto load_a = [&](floatx4(&a)[CB], int it) {
     if (it >= n_it) it = n_it - 1;  // tail prefetch: a valid address, never consumed
     const float* ap = aptr + (int64_t)it * wstep;
-    a[0] = *(const floatx4*)ap;
-    a[1] = *(const floatx4*)(ap + 256);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) a[cb] = *(const floatx4*)(ap + cb * 256);
   };
   // the B operands of k step `it` (chunk c, tap t) from LDS
   auto read_b = [&](floatx4(&b)[2], int it) {
@@ -119,11 +119,11 @@ __global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, C
   };
   // one k step: 16 MFMAs in conv_mfma_f32's order (round 5: reading the B operands one step ahead
   // measured slower, 431 -> 408 frames/s on the fp32 line: profiles/r05/ab_r05e_fp32_b_prefetch_not_kept.log)
-  auto mma = [&](const floatx4(&a)[2], const floatx4(&b)[2]) {
+  auto mma = [&](const floatx4(&a)[CB], const floatx4(&b)[2]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
         for (int pb = 0; pb < 2; ++pb)
           acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][j], b[pb][j], acc[cb][pb], 0, 0, 0);
@@ -142,11 +142,11 @@ __global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, C
   };
 
   issue_halo(0, 0);
-  floatx4 a0[2], a1[2];
+  floatx4 a0[CB], a1[CB];
   load_a(a0, 0);
   load_a(a1, 1);
   int it = 0;
-  auto step = [&](const floatx4(&a)[2], int it) {
+  auto step = [&](const floatx4(&a)[CB], int it) {
     floatx4 b[2];
     read_b(b, it);
     mma(a, b);
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, C
     if (y >= s.h || x >= s.w) continue;
     float* optr = g.out + ((int64_t)(frame * hp_out + y + s.pout) * wp_out + (x + s.pout)) * s.cs_out;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
+    for (int cb = 0; cb < CB; ++cb) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int co = co_base + cb * 32 + 8 * q + 4 * hi;
@@ -195,23 +195,32 @@ __global__ __launch_bounds__(256) void conv_f32_lds(ConvShape s, ConvGroup g0, C
   }
 }
 
-template <int KS, int TCW>
-static int launch_f32_lds_t(const ConvShape& s, const ConvGroup* g, hipStream_t st) {
+template <int KS, int TCW, int CB>
+static int launch_f32_lds_cb(const ConvShape& s, const ConvGroup* g, hipStream_t st) {
   using T = F32Tile<KS, TCW>;
   static bool attr = false;
   if (!attr) {
-    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_f32_lds<KS, TCW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_f32_lds<KS, TCW, CB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      T::LDS));
     attr = true;
   }
   const int tiles_x = (s.w + TCW - 1) / TCW, tiles_y = (s.h + T::TR - 1) / T::TR;
   const int cop_max = s.groups > 1 ? std::max(g[0].cop, g[1].cop) : g[0].cop;
-  const dim3 grid((unsigned)(s.n * tiles_x * tiles_y), (unsigned)((cop_max + 63) / 64), (unsigned)s.groups);
-  hipLaunchKernelGGL((conv_f32_lds<KS, TCW>), grid, dim3(256), T::LDS, st, s, g[0], s.groups > 1 ? g[1] : g[0],
+  const dim3 grid((unsigned)(s.n * tiles_x * tiles_y), (unsigned)((cop_max + CB * 32 - 1) / (CB * 32)), (unsigned)s.groups);
+  hipLaunchKernelGGL((conv_f32_lds<KS, TCW, CB>), grid, dim3(256), T::LDS, st, s, g[0], s.groups > 1 ? g[1] : g[0],
                      tiles_x, tiles_y);
   OP_AFTER_LAUNCH("conv_f32_lds", st);
   OP_HIP_CHECK(hipGetLastError());
   return OP_OK;
+}
+
+template <int KS, int TCW>
+static int launch_f32_lds_t(const ConvShape& s, const ConvGroup* g, hipStream_t st) {
+  // OP_F32_CB=4: 128 output channels per wave (A/B aid, read per call; needs cop % 128 == 0)
+  const char* e = getenv("OP_F32_CB");
+  bool cb4 = e && atoi(e) == 4;
+  for (int i = 0; i < s.groups; ++i) cb4 = cb4 && g[i].cop % 128 == 0;
+  return cb4 ? launch_f32_lds_cb<KS, TCW, 4>(s, g, st) : launch_f32_lds_cb<KS, TCW, 2>(s, g, st);
 }
 
 // 3x3 / 7x7 on the LDS-halo kernel; *taken = 0 when the shape is outside it (conv_mfma_f32 runs).

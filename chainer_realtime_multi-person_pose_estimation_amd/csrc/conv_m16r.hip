@@ -163,9 +163,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
     const bool next = cp + 1 < ncp;
     // B fragments one 16-px block ahead, across tap boundaries (the first block of tap t + 1 is
     // read during the last block of tap t)
-    bf16x8g bh[2], bl[2];
-    bh[0] = *(const bf16x8g*)hb;
-    bl[0] = *(const bf16x8g*)(hb + HPLANE);
+    // B fragments one block ahead (round 5: two blocks ahead, three register sets, measured neutral:
+    // profiles/r05/ab_r05j_m16r_b_two_ahead_neutral.log)
+    constexpr int NBB = 2;
+    auto boff = [&](int idx) {  // byte offset of block idx's B fragment (compile-time after unrolling)
+      const int t1 = idx / NPX, pb1 = idx % NPX;
+      return (((t1 / 3) + pb1 / TCB) * PITCH + (t1 % 3) + (pb1 % TCB) * 16) * 16;
+    };
+    bf16x8g bh[NBB], bl[NBB];
+#pragma unroll
+    for (int k = 0; k < NBB - 1; ++k) {
+      bh[k] = *(const bf16x8g*)(hb + boff(k));
+      bl[k] = *(const bf16x8g*)(hb + boff(k) + HPLANE);
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int it = cp * 9 + t;
@@ -177,12 +187,11 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_m16r_bf16x3(SplitConvShape s,
       const AFrag& a = abuf[(9 * P + t) % NB];
 #pragma unroll
       for (int pb = 0; pb < NPX; ++pb) {
-        const int idx = t * NPX + pb, cur = idx & 1;
-        if (idx + 1 < 9 * NPX) {
-          const int t1 = (idx + 1) / NPX, pb1 = (idx + 1) % NPX;
-          const int o1 = (((t1 / 3) + pb1 / TCB) * PITCH + (t1 % 3) + (pb1 % TCB) * 16) * 16;
-          bh[cur ^ 1] = *(const bf16x8g*)(hb + o1);
-          bl[cur ^ 1] = *(const bf16x8g*)(hb + o1 + HPLANE);
+        const int idx = t * NPX + pb, cur = idx % NBB;
+        if (idx + NBB - 1 < 9 * NPX) {
+          const int o1 = boff(idx + NBB - 1);
+          bh[(idx + NBB - 1) % NBB] = *(const bf16x8g*)(hb + o1);
+          bl[(idx + NBB - 1) % NBB] = *(const bf16x8g*)(hb + o1 + HPLANE);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

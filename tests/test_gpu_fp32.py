@@ -41,6 +41,19 @@ def test_lds_kernel_bit_identical_to_global_load_kernel(lib, f32ctx, monkeypatch
         assert a.shape == b.shape and np.array_equal(a, b), float(np.abs(a - b).max())
 
 
+def test_lds_kernel_128_channel_waves_bit_identical(lib, f32ctx, monkeypatch):
+    """OP_F32_CB=4 (A/B aid): 128 output channels per wave, the same per-output k order."""
+    rng = np.random.default_rng(31)
+    x = rng.uniform(-0.5, 0.5, (2, 3, 184, 200)).astype(np.float32)
+    out = {}
+    for cb in ("4", "2"):
+        monkeypatch.setenv("OP_F32_CB", cb)
+        out[cb] = f32ctx.forward(x)
+    monkeypatch.delenv("OP_F32_CB")
+    for a, b in zip(out["4"], out["2"]):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
 def test_lds_kernel_vs_oracle(f32ctx, rand_weights):
     rng = np.random.default_rng(7)
     x = rng.uniform(-0.5, 0.5, (1, 3, 96, 112)).astype(np.float32)
