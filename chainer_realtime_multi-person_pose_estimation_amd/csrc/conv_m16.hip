@@ -38,20 +38,29 @@ __device__ unsigned long long g_m16_st[12];
 // of 4 slots / 1 pair.  A small tile's workgroup does little MFMA work per tap pair, so with one pair
 // of prefetch it waits on the weight fetch (L2 / HBM latency) every pair: the single-frame and
 // single-crop launches.
-template <int KS, int NPX, bool DEEP = false>
+// STAG (round 5): the two waves of a SIMD run half a tap pair apart.  Waves 0-3 (which stage the
+// ring) meet the ring barrier at the start of their pair p, waves 4-7 in the middle of their pair
+// p - 1 (after block NPX / 2), so when one half starts a pair -- vmcnt wait, barrier, DMA issue, A / B
+// fragment reads, the 28 % of a wave's time before its first MFMA (profiles/r05/m16_stamps_*) -- its
+// SIMD partner is halfway through its MFMA stream.  The ring then holds three pairs (the one each
+// half reads and the one being staged: 6 taps, 48 KiB), so the halo planes shrink to 28 KiB
+// (launch_m16_7x7 takes it where nh <= 28, e.g. the 46 x 46 batch rasters at 27).
+template <int KS, int NPX, bool DEEP = false, bool STAG = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
+  static_assert(!(DEEP && STAG), "the staggered ring is for the 32-KiB-plane form");
   constexpr int KSQ = KS * KS;
   constexpr int R = KS / 2;
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
   constexpr int PLANE_W = CW * 16;
   constexpr int SLOT_W = 4 * PLANE_W;
-  constexpr int RING = DEEP ? 12 : 4;    // taps; even, so a pair never wraps
-  constexpr int AHEAD = RING / 2 - 1;    // tap pairs staged ahead of the one being computed
+  constexpr int RING = DEEP ? 12 : (STAG ? 6 : 4);  // taps; even, so a pair never wraps
+  constexpr int AHEAD = STAG ? 1 : RING / 2 - 1;    // tap pairs staged ahead of the one being computed
   constexpr int CAP = PG * NPX * 16;
-  // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16), placed first so a
-  // lane's lo-plane read is its hi-plane address + an immediate offset; the weight ring follows
-  constexpr int HPLANE = (DEEP ? 16 : 32) * 1024;
+  // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16; STAG: nh <= 28),
+  // placed first so a lane's lo-plane read is its hi-plane address + an immediate offset; the
+  // weight ring follows
+  constexpr int HPLANE = (DEEP ? 16 : (STAG ? 28 : 32)) * 1024;
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
 
   const int lin = blockIdx.x;
@@ -252,7 +261,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         __builtin_amdgcn_sched_barrier(0);
 #endif
 #if !M16_PROBE_NOBAR  // timing probe only (racy ring): no per-pair barrier
-        __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
+        if (!STAG) {
+          __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
+        } else if (wave < 4 && t > 0) {
+          // waves 0-3 at the start of pair p, waves 4-7 in the middle of pair p - 1 (below): pair p's
+          // pieces landed for every wave; pair p - 2's slot (the one staged next) is free -- waves
+          // 4-7 read pair p - 2 before their previous barrier.  The chunk's first pair needs none:
+          // the chunk barriers above ordered everything
+          __builtin_amdgcn_s_barrier();
+        }
 #endif
         asm volatile("" ::: "memory");
 #if M16_STAMPS
@@ -288,6 +305,12 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #pragma unroll
         for (int pb = 0; pb < NPX; ++pb) {
           const int cur = pb & 1;
+          if (STAG && pb == NPX / 2 && wave >= 4 && t + 2 < kPairsEnd) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();  // waves 0-3's barrier at the start of pair p + 1 (above)
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+          }
           if (pb + 1 < NPX) {
             const char* bp = halo + qb[pb + 1] + toff;
             bh[cur ^ 1] = *(const bf16x8g*)bp;
@@ -392,7 +415,12 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 5>,  (const void*)conv_m16_bf16x3<7, 4>,
                          (const void*)conv_m16_bf16x3<7, 3>,  (const void*)conv_m16_bf16x3<7, 2>,
                          (const void*)conv_m16_bf16x3<7, 5, true>, (const void*)conv_m16_bf16x3<7, 4, true>,
-                         (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>};
+                         (const void*)conv_m16_bf16x3<7, 3, true>, (const void*)conv_m16_bf16x3<7, 2, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, true>, (const void*)conv_m16_bf16x3<7, 9, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, true>, (const void*)conv_m16_bf16x3<7, 7, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, true>, (const void*)conv_m16_bf16x3<7, 5, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 4, false, true>, (const void*)conv_m16_bf16x3<7, 3, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 2, false, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -405,34 +433,41 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   // small tiles whose halo planes fit 16 KiB take the deep weight ring (12 taps, 5 pairs ahead)
   static const bool no_deep = getenv("OP_M16_NODEEP") && atoi(getenv("OP_M16_NODEEP")) != 0;  // A/B aid
   const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
+  // the staggered halves where the halo planes fit 28 KiB (OP_M16_STAG=0: off; read per call)
+  const char* stag_env = getenv("OP_M16_STAG");
+  const bool stag = !deep && tl.nh <= 28 && M16_DMA_HALF && !(stag_env && atoi(stag_env) == 0);
   const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
-                       : 4 * 4 * 128 * 16 + 4 * 32 * 1024;   // ring + 4 halo planes (32-KiB stride)
+                  : stag ? 6 * 4 * 128 * 16 + 4 * 28 * 1024  // 6-tap ring + 4 planes (28-KiB stride)
+                         : 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes (32-KiB stride)
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu * std::max(tl.pair, 1))
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
+#define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
+#define M16_CASE(N)                  \
+  case N:                            \
+    if (deep && N <= 5)              \
+      M16_LAUNCH(N, (N <= 5), false); \
+    else if (stag)                   \
+      M16_LAUNCH(N, false, true);    \
+    else                             \
+      M16_LAUNCH(N, false, false);   \
+    break;
   switch (npx) {
-    case 9: hipLaunchKernelGGL((conv_m16_bf16x3<7, 9>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-    case 8: hipLaunchKernelGGL((conv_m16_bf16x3<7, 8>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-    case 7: hipLaunchKernelGGL((conv_m16_bf16x3<7, 7>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-    case 6: hipLaunchKernelGGL((conv_m16_bf16x3<7, 6>), grid, dim3(512), lds, st, s, g0, g1, tl); break;
-    case 5:
-      if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 5, true>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      else hipLaunchKernelGGL((conv_m16_bf16x3<7, 5>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      break;
-    case 4:
-      if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 4, true>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      else hipLaunchKernelGGL((conv_m16_bf16x3<7, 4>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      break;
-    case 3:
-      if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 3, true>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      else hipLaunchKernelGGL((conv_m16_bf16x3<7, 3>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      break;
-    case 2:
-      if (deep) hipLaunchKernelGGL((conv_m16_bf16x3<7, 2, true>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      else hipLaunchKernelGGL((conv_m16_bf16x3<7, 2>), grid, dim3(512), lds, st, s, g0, g1, tl);
-      break;
-    default: hipLaunchKernelGGL((conv_m16_bf16x3<7, 10>), grid, dim3(512), lds, st, s, g0, g1, tl);
+    M16_CASE(9)
+    M16_CASE(8)
+    M16_CASE(7)
+    M16_CASE(6)
+    M16_CASE(5)
+    M16_CASE(4)
+    M16_CASE(3)
+    M16_CASE(2)
+    default:
+      if (stag) M16_LAUNCH(10, false, true);
+      else M16_LAUNCH(10, false, false);
   }
+#undef M16_CASE
+#undef M16_LAUNCH
+  census_add(stag ? OP_CENSUS_7X7_STAG : OP_CENSUS_7X7_PLAIN_RING);
 #if M16_STAMPS
   static const bool dump = getenv("OP_M16_STAMPS") != nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

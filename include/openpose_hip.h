@@ -307,6 +307,8 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_CUBIC_ROWS 28  /* two-pass second resize as one row-block launch for the batch
                                     (resize_cubic_f32_planar_mean_rows), else one launch per frame */
 #define OP_CENSUS_F32_LDS 29     /* exact-f32 3x3 / 7x7 launches on the LDS-halo kernel conv_f32_lds (round 5) */
+#define OP_CENSUS_7X7_STAG 30       /* conv_m16 7x7 launches with the staggered halves (round 5) */
+#define OP_CENSUS_7X7_PLAIN_RING 31 /* ... with one ring barrier per pair for all 8 waves */
 #define OP_CENSUS_SLOTS 32
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

@@ -294,3 +294,28 @@ def test_planar_stage_layout_is_bit_identical(lib, bctx, n):
             bctx.set_stage_layout(1)
         assert cen["7x7_planar"] == (25 if planar else 0), (planar, cen)
     assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
+
+
+@pytest.mark.parametrize("n", [1, 38, 232])
+def test_staggered_halves_bit_identical(lib, bctx, monkeypatch, n):
+    """Round 5: the 7x7 kernel's staggered halves (waves 0-3 meet the ring barrier at a pair's start,
+    waves 4-7 in its middle; OP_M16_STAG=0 restores one barrier per pair for all 8 waves) move only
+    when each wave waits, not what it accumulates: the maps are bit-identical at 38 and the
+    headline's 232 frames; the census shows which ring ran (one frame: the deep ring, unstaggered)."""
+    rng = np.random.default_rng(900 + n)
+    x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
+    out = {}
+    for stag in ("1", "0"):
+        monkeypatch.setenv("OP_M16_STAG", stag)
+        _census_npx(lib)
+        out[stag] = bctx.forward(x)
+        cen = _census_npx(lib)
+        print("n %d OP_M16_STAG=%s census:" % (n, stag), cen)
+        if stag == "1":
+            # one frame's small split-K tiles take the deep 12-tap ring, which is never staggered
+            assert cen["7x7_stag"] == (25 if n > 1 else 0), cen
+        else:
+            assert cen["7x7_stag"] == 0 and cen["7x7_plain_ring"] == 25, cen
+    monkeypatch.delenv("OP_M16_STAG")
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
