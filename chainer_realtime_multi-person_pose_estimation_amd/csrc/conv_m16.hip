@@ -42,20 +42,23 @@ __device__ unsigned long long g_m16_st[12];
 // ring) meet the ring barrier at the start of their pair p, waves 4-7 in the middle of their pair
 // p - 1 (after block NPX / 2), so when one half starts a pair -- vmcnt wait, barrier, DMA issue, A / B
 // fragment reads, the 28 % of a wave's time before its first MFMA (profiles/r05/m16_stamps_*) -- its
-// SIMD partner is halfway through its MFMA stream.  The ring then holds three pairs (the one each
-// half reads and the one being staged: 6 taps, 48 KiB), so the halo planes shrink to 28 KiB
-// (launch_m16_7x7 takes it where nh <= 28, e.g. the 46 x 46 batch rasters at 27).
+// SIMD partner is halfway through its MFMA stream.  The slot staged at the barrier held pair p - 1,
+// whose A fragments waves 4-7 read into registers when they started it, so the 4-tap ring would
+// do; measured, the 32-KiB-plane form is faster with a 6-tap ring (three pair slots) in 28-KiB halo
+// planes (7x7 -1.8 %, profiles/r05/ab_r05l_*) than with the 4-tap ring (+1.4 %, ab_r05o_*), so it
+// takes that where nh <= 28 (the 46 x 46 batch rasters: 27); the deep 12-tap ring (small tiles:
+// one frame's split-K launches) is staggered as it is (one frame's 7x7 -4.7 %).
 template <int KS, int NPX, bool DEEP = false, bool STAG = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
-  static_assert(!(DEEP && STAG), "the staggered ring is for the 32-KiB-plane form");
+  static_assert(!STAG || M16_DMA_HALF, "staggered halves: waves 4-7 must not stage the ring");
   constexpr int KSQ = KS * KS;
   constexpr int R = KS / 2;
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
   constexpr int PLANE_W = CW * 16;
   constexpr int SLOT_W = 4 * PLANE_W;
   constexpr int RING = DEEP ? 12 : (STAG ? 6 : 4);  // taps; even, so a pair never wraps
-  constexpr int AHEAD = STAG ? 1 : RING / 2 - 1;    // tap pairs staged ahead of the one being computed
+  constexpr int AHEAD = DEEP ? 5 : 1;               // tap pairs staged ahead of the one being computed
   constexpr int CAP = PG * NPX * 16;
   // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16; STAG: nh <= 28),
   // placed first so a lane's lo-plane read is its hi-plane address + an immediate offset; the
@@ -265,9 +268,9 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
           __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
         } else if (wave < 4 && t > 0) {
           // waves 0-3 at the start of pair p, waves 4-7 in the middle of pair p - 1 (below): pair p's
-          // pieces landed for every wave; pair p - 2's slot (the one staged next) is free -- waves
-          // 4-7 read pair p - 2 before their previous barrier.  The chunk's first pair needs none:
-          // the chunk barriers above ordered everything
+          // pieces landed for every wave; the slot staged next (pair p - 1's) is free -- waves 4-7
+          // hold pair p - 1's A fragments in registers since they started it.  The chunk's first
+          // pair needs none: the chunk barriers above ordered everything
           __builtin_amdgcn_s_barrier();
         }
 #endif
@@ -420,7 +423,9 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 8, false, true>, (const void*)conv_m16_bf16x3<7, 7, false, true>,
                          (const void*)conv_m16_bf16x3<7, 6, false, true>, (const void*)conv_m16_bf16x3<7, 5, false, true>,
                          (const void*)conv_m16_bf16x3<7, 4, false, true>, (const void*)conv_m16_bf16x3<7, 3, false, true>,
-                         (const void*)conv_m16_bf16x3<7, 2, false, true>};
+                         (const void*)conv_m16_bf16x3<7, 2, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 5, true, true>, (const void*)conv_m16_bf16x3<7, 4, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 3, true, true>, (const void*)conv_m16_bf16x3<7, 2, true, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -433,9 +438,9 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   // small tiles whose halo planes fit 16 KiB take the deep weight ring (12 taps, 5 pairs ahead)
   static const bool no_deep = getenv("OP_M16_NODEEP") && atoi(getenv("OP_M16_NODEEP")) != 0;  // A/B aid
   const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
-  // the staggered halves where the halo planes fit 28 KiB (OP_M16_STAG=0: off; read per call)
+  // the staggered halves (OP_M16_STAG=0: one barrier per pair for all 8 waves; read per call)
   const char* stag_env = getenv("OP_M16_STAG");
-  const bool stag = !deep && tl.nh <= 28 && M16_DMA_HALF && !(stag_env && atoi(stag_env) == 0);
+  const bool stag = M16_DMA_HALF && (deep || tl.nh <= 28) && !(stag_env && atoi(stag_env) == 0);
   const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
                   : stag ? 6 * 4 * 128 * 16 + 4 * 28 * 1024  // 6-tap ring + 4 planes (28-KiB stride)
                          : 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes (32-KiB stride)
@@ -443,14 +448,16 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
-#define M16_CASE(N)                  \
-  case N:                            \
-    if (deep && N <= 5)              \
-      M16_LAUNCH(N, (N <= 5), false); \
-    else if (stag)                   \
-      M16_LAUNCH(N, false, true);    \
-    else                             \
-      M16_LAUNCH(N, false, false);   \
+#define M16_CASE(N)                                  \
+  case N:                                            \
+    if (deep && N <= 5) {                            \
+      if (stag) M16_LAUNCH(N, (N <= 5), true);       \
+      else M16_LAUNCH(N, (N <= 5), false);           \
+    } else if (stag) {                               \
+      M16_LAUNCH(N, false, true);                    \
+    } else {                                         \
+      M16_LAUNCH(N, false, false);                   \
+    }                                                \
     break;
   switch (npx) {
     M16_CASE(9)

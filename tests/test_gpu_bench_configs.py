@@ -301,7 +301,8 @@ def test_staggered_halves_bit_identical(lib, bctx, monkeypatch, n):
     """Round 5: the 7x7 kernel's staggered halves (waves 0-3 meet the ring barrier at a pair's start,
     waves 4-7 in its middle; OP_M16_STAG=0 restores one barrier per pair for all 8 waves) move only
     when each wave waits, not what it accumulates: the maps are bit-identical at 38 and the
-    headline's 232 frames; the census shows which ring ran (one frame: the deep ring, unstaggered)."""
+    headline's 232 frames and at one frame (split-K tiles on the deep 12-tap ring); the census shows
+    which ring ran."""
     rng = np.random.default_rng(900 + n)
     x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
     out = {}
@@ -312,10 +313,41 @@ def test_staggered_halves_bit_identical(lib, bctx, monkeypatch, n):
         cen = _census_npx(lib)
         print("n %d OP_M16_STAG=%s census:" % (n, stag), cen)
         if stag == "1":
-            # one frame's small split-K tiles take the deep 12-tap ring, which is never staggered
-            assert cen["7x7_stag"] == (25 if n > 1 else 0), cen
+            assert cen["7x7_stag"] == 25, cen  # one frame: the deep 12-tap ring, staggered too
         else:
             assert cen["7x7_stag"] == 0 and cen["7x7_plain_ring"] == 25, cen
     monkeypatch.delenv("OP_M16_STAG")
     for a, b in zip(out["1"], out["0"]):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
+def test_staggered_halves_precise_720p(lib, monkeypatch):
+    """The staggered 7x7 halves on the multi-scale path's wide maps (41- to 164-column maps, halo
+    planes up to 32 KiB, frame-aligned and tight-pitch raster tiles): 2 frames of 1280x720 through
+    run_staged_precise give bit-identical averaged maps with OP_M16_STAG=1 and 0."""
+    from test_gpu_precise_full import _crowd_frame, _weights
+    frames = np.stack([_crowd_frame(41), _crowd_frame(42)])
+    c = lib.Context(0)
+    try:
+        c.set_weights(_weights(case_weights("posenet", 0)))
+        out = {}
+        for stag in ("1", "0"):
+            monkeypatch.setenv("OP_M16_STAG", stag)
+            c.stage_frames(frames)
+            _census_npx(lib)
+            try:
+                c.run_staged_precise()
+            except IndexError:
+                pass
+            c.synchronize()
+            cen = _census_npx(lib)
+            if stag == "1":  # the launches whose halo planes fit 28 KiB (and every deep-ring launch)
+                assert cen["7x7_stag"] > 0, cen
+            else:
+                assert cen["7x7_stag"] == 0 and cen["7x7_plain_ring"] == 4 * 25, cen
+            out[stag] = c.fetch_maps(0, 2)
+        monkeypatch.delenv("OP_M16_STAG")
+        for a, b in zip(out["1"], out["0"]):
+            assert np.array_equal(a, b), float(np.abs(a - b).max())
+    finally:
+        c.close()
