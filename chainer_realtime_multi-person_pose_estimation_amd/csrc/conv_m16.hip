@@ -440,7 +440,9 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   const bool deep = npx <= 5 && tl.nh <= 16 && !no_deep;
   // the staggered halves (OP_M16_STAG=0: one barrier per pair for all 8 waves; read per call)
   const char* stag_env = getenv("OP_M16_STAG");
-  const bool stag = M16_DMA_HALF && (deep || tl.nh <= 28) && !(stag_env && atoi(stag_env) == 0);
+  // not on frame-aligned raster tiles (the wide multi-scale maps): C4's 7x7 79.2 ms staggered
+  // everywhere, 78.5 never, 77.8 except those (profiles/r05/ab_r05p_7x7_stag_c4_modes.log)
+  const bool stag = M16_DMA_HALF && (deep || tl.nh <= 28) && tl.fa_tiles == 0 && !(stag_env && atoi(stag_env) == 0);
   const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
                   : stag ? 6 * 4 * 128 * 16 + 4 * 28 * 1024  // 6-tap ring + 4 planes (28-KiB stride)
                          : 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes (32-KiB stride)
