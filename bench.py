@@ -400,16 +400,17 @@ def bench_line(args, L, Wm, Fr, transport, rank, world, local):
         else:
             peak = FP32_MATRIX_PEAK_TFLOPS
             kern = "conv_mfma_f32<7,2,2> (7x7 stage convs, v_mfma_f32_32x32x2_f32)"
-        if args.precision == "bf16x3":
-            # the 7x7 kernel this workload actually ran (launch census of one extra step)
-            L.conv_census(reset=True)
-            run.step(False)
-            run.drain()
-            ctx.synchronize()
-            cen = L.conv_census(reset=True)
-            if cen["npx"]:
-                kern = "conv_m16_bf16x3<7, %d> (7x7 stage convs, 3xBF16 split on v_mfma_f32_16x16x32_bf16)" % max(
-                    cen["npx"], key=cen["npx"].get)
+        # the 7x7 kernel this workload actually ran (launch census of one extra step)
+        L.conv_census(reset=True)
+        run.step(False)
+        run.drain()
+        ctx.synchronize()
+        cen = L.conv_census(reset=True)
+        if args.precision == "bf16x3" and cen["npx"]:
+            kern = "conv_m16_bf16x3<7, %d> (7x7 stage convs, 3xBF16 split on v_mfma_f32_16x16x32_bf16)" % max(
+                cen["npx"], key=cen["npx"].get)
+        elif args.precision != "bf16x3" and cen["f32_lds"]:
+            kern = "conv_f32_lds<7, 16> (7x7 stage convs, LDS halo, v_mfma_f32_32x32x2_f32)"
         traffic, tsrc = committed_traffic(kern.split(" ")[0], B, args.precision, halo_mode)
         roofline = {"bound": "mfma", "kernel": kern,
                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
