@@ -329,7 +329,7 @@ def batch1_line(L, ctx, low, FH, FW, steps=60, warmup=10):
         ctx.run_staged()
         ctx.synchronize()
         cen = L.conv_census(reset=True)
-        out["conv7x7_tiles"] = {"npx": cen["npx"], "splitk_launches": cen["7x7_splitk"]}
+        out["conv7x7_tiles"] = {"npx": cen["npx"], "splitk_launches": cen["7x7_splitk"], "m16q_launches": cen["7x7_q"]}
         out["note"] = ("one %dx%d frame per synchronous call: upload, run_staged, fetch_results; median of %d "
                        "calls after %d warm-up" % (FW, FH, steps, warmup))
     finally:

@@ -845,6 +845,66 @@ bool conv_m16_takes(int n, int h, int w, int groups, int cop_max) {
   return cop_max % 128 == 0 && raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, n, h, w, groups, cop_max, tl, true);
 }
 
+// Small 7x7 launches (round 5): conv_m16q_bf16x3 (conv_m16q.hip) where split-K is allowed and the
+// launch covers at most OP_M16Q_MAX_PX pixels (default 4800: one 368x368 frame's 46 x 46 maps, not
+// C4's or C5's batches); OP_M16Q=0 (read per launch) keeps them on conv_m16.  Tiles of OP_M16Q_TR
+// rows (2 / 4 / 8; default 4) x 16 columns, split K over the chunk pairs x OP_M16Q_NTH tap ranges
+// (2..4, default 2, lowered until the splits fit kMaxSplitK), weights OP_M16Q_PF (2 / 4, default 2)
+// taps ahead; the partials go through conv_m16_splitk_reduce like conv_m16's.  One frame's 7x7
+// class 1.02 -> 0.95 ms (TR 2 / 8, NTH 3 / 4, PF 4 / 6 no better: profiles/r05/ab_r05s_*.log).
+// *taken = 0 when the launch is outside it.
+static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, int cop_max, hipStream_t st,
+                            int* taken) {
+  *taken = 0;
+  const char* on = getenv("OP_M16Q");
+  if ((on && atoi(on) == 0) || !s.splitk || s.ks != 7 || s.pin < 3 || (s.c16 & 1) || cop_max % 128) return OP_OK;
+  static const int64_t max_px = getenv("OP_M16Q_MAX_PX") ? atoll(getenv("OP_M16Q_MAX_PX")) : 4800;
+  if ((int64_t)s.n * s.h * s.w > max_px) return OP_OK;
+  for (int i = 0; i < s.groups; ++i)
+    if (g[i].cop % 128 || g[i].cin_off % 16) return OP_OK;
+  const char* tr_env = getenv("OP_M16Q_TR");  // (read per launch: A/B and test aids)
+  const char* nth_env = getenv("OP_M16Q_NTH");
+  const char* pf_env = getenv("OP_M16Q_PF");
+  const int tr = tr_env ? atoi(tr_env) : 4;
+  const int nth0 = nth_env ? atoi(nth_env) : 2;
+  const int pf = pf_env ? atoi(pf_env) : 2;
+  if (tr != 2 && tr != 4 && tr != 8) return OP_OK;
+  const int ncp = s.c16 / 2;
+  // the instantiated kernels: TR 4 with 2..4 tap ranges and prefetch 2 / 4; TR 2 / 8 with 2 and 2
+  int nth = tr == 4 ? std::max(2, std::min(nth0, 4)) : 2;
+  const int pfk = tr == 4 && pf == 4 ? 4 : 2;
+  while (nth > 2 && ncp * nth > kMaxSplitK) --nth;
+  if (ncp * nth > kMaxSplitK) return OP_OK;
+  BigTiling t{};
+  t.tr = tr;
+  t.tc = 16;
+  t.tiles_x = (s.w + 15) / 16;
+  t.tiles_y = (s.h + tr - 1) / tr;
+  t.co_tiles = cop_max / 128;
+  t.units = s.groups * t.co_tiles;
+  t.per_unit = s.n * t.tiles_y * t.tiles_x;
+  t.hw = s.h * s.w;
+  t.total = s.n * t.hw;
+  t.ksplit = ncp * nth;
+  float* ws = splitk_ws(st, (size_t)t.ksplit * s.groups * t.total * cop_max);
+  if (!ws) return OP_OK;  // capturing with a short workspace: conv_m16 unsplit now, re-captured later
+  t.ws = ws;
+  *taken = 1;
+  census_add(OP_CENSUS_7X7_Q);
+  census_add(OP_CENSUS_7X7_SPLITK);
+  if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
+  const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
+  const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t);
+  if (rc != OP_OK) return rc;
+  OP_AFTER_LAUNCH("conv_m16q_bf16x3", st);
+  const int64_t items = (int64_t)t.total * (cop_max / 4);
+  hipLaunchKernelGGL(conv_m16_splitk_reduce, dim3((unsigned)((items + 255) / 256), (unsigned)s.groups), dim3(256), 0,
+                     st, s, g[0], g1, t);
+  OP_AFTER_LAUNCH("conv_m16_splitk_reduce", st);
+  OP_HIP_CHECK(hipGetLastError());
+  return OP_OK;
+}
+
 int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_t st, int* taken) {
   *taken = 0;
   if ((s.ks != 7 && s.ks != 3) || s.cs_in % 16 || s.pin < s.ks / 2) return OP_OK;
@@ -859,6 +919,10 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   BigTiling tl{};
   if (s.ks == 7) {
     if (!c128) return OP_OK;
+    {
+      const int rc = launch_conv_m16q(s, g, cop_max, st, taken);
+      if (rc != OP_OK || *taken) return rc;
+    }
     if (raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
       // default: 16x16x32 tap pairs on raster tiles, 10 blocks of 16 px per wave = the 640-px tile of npb 5
       // Tile size per launch shape.  A workgroup's time grows as ~(2 + NPX) (fixed halo /

@@ -142,5 +142,9 @@ int launch_conv_m16r(const SplitConvShape& s, const SplitConvGroup* g, bool pool
 
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl);
+// conv_m16q.hip: the small-launch 7x7 kernel (tr x 16 tiles, split K over chunk pairs x nth tap
+// ranges, f32 partials in tl.ws for conv_m16_splitk_reduce)
+int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
+                    const SplitConvGroup& g1, const BigTiling& tl);
 
 }  // namespace op

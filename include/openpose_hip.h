@@ -309,7 +309,8 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_F32_LDS 29     /* exact-f32 3x3 / 7x7 launches on the LDS-halo kernel conv_f32_lds (round 5) */
 #define OP_CENSUS_7X7_STAG 30       /* conv_m16 7x7 launches with the staggered halves (round 5) */
 #define OP_CENSUS_7X7_PLAIN_RING 31 /* ... with one ring barrier per pair for all 8 waves */
-#define OP_CENSUS_SLOTS 32
+#define OP_CENSUS_7X7_Q 32          /* 7x7 launches on the small-launch kernel conv_m16q_bf16x3 (round 5) */
+#define OP_CENSUS_SLOTS 40
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 
 /* Algorithmic FLOPs of the forward for one frame of net size h x w (2*Ci*Co*k*k*H*W summed). */

@@ -305,6 +305,7 @@ def test_staggered_halves_bit_identical(lib, bctx, monkeypatch, n):
     which ring ran."""
     rng = np.random.default_rng(900 + n)
     x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
+    monkeypatch.setenv("OP_M16Q", "0")  # one frame: conv_m16's split-K tiles, not conv_m16q
     out = {}
     for stag in ("1", "0"):
         monkeypatch.setenv("OP_M16_STAG", stag)
@@ -327,6 +328,7 @@ def test_staggered_halves_precise_720p(lib, monkeypatch):
     run_staged_precise give bit-identical averaged maps with OP_M16_STAG=1 and 0."""
     from test_gpu_precise_full import _crowd_frame, _weights
     frames = np.stack([_crowd_frame(41), _crowd_frame(42)])
+    monkeypatch.setenv("OP_M16Q", "0")  # the smallest scale's launch (<= 4800 px) stays on conv_m16
     c = lib.Context(0)
     try:
         c.set_weights(_weights(case_weights("posenet", 0)))

@@ -1,6 +1,7 @@
 """Interleaved A/B of library builds (OP_LIB_VARIANT) or environment settings with per-class times:
 each variant runs in its own child process per round (a process loads one library).
-usage: ab_lib.py ROUNDS base v1 NAME=VALUE[,NAME=VALUE] ...  (an '=' spec sets env vars, product lib)
+usage: ab_lib.py ROUNDS base v1 NAME=VALUE[,NAME=VALUE] v1,NAME=VALUE ...  (NAME=VALUE parts set env
+vars; a bare part picks the library variant, else the product library)
 AB_BENCH_ARGS: extra bench.py arguments (e.g. "--precise --frame 720x1280 --steps 5")."""
 import json
 import os
@@ -13,10 +14,11 @@ here = os.path.dirname(os.path.abspath(__file__))
 out = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
-        if "=" in v:
-            env = dict(os.environ, OP_LIB_VARIANT="", **dict(kv.split("=", 1) for kv in v.split(",")))
-        else:
-            env = dict(os.environ, OP_LIB_VARIANT="" if v == "base" else v)
+        # comma-separated parts: NAME=VALUE sets an env var, a bare name picks the library variant
+        parts = v.split(",")
+        libs = [x for x in parts if "=" not in x and x != "base"]
+        env = dict(os.environ, OP_LIB_VARIANT=libs[0] if libs else "",
+                   **dict(kv.split("=", 1) for kv in parts if "=" in kv))
         p = subprocess.run([sys.executable, os.path.join(here, "..", "bench.py"), "--no-cpu-baseline", "--no-variants", "--steps", "10",
                             "--warmup", "2"] + os.environ.get("AB_BENCH_ARGS", "").split(), env=env, capture_output=True,
                            text=True, timeout=300)
