@@ -27,7 +27,8 @@
 // of its six MFMAs per block removed it still took ~80 % of the time, and without the per-tap
 // weight loads or with every tap reading tap 0's pixels ~97 %; its workgroups (2-3 per CU, all
 // resident) spend 84 % in the tap loop at ~1800 cycles per tap per wave against 384 of MFMA issue.
-// Prefetch 2 / 4 / 6 taps ahead and product-major MFMA order measured within noise.
+// Prefetch 2 / 4 / 6 taps ahead, product-major MFMA order, a cap of 3 workgroups per CU and a
+// rolled tap loop (a tenth of the code) measured within noise.
 //
 // Launch contract (launch_conv_m16q in conv_big.hip checks it): ks = 7, pin >= 3, c16 even, every
 // group's cop a multiple of 128, tl.ksplit = (c16 / 2) * nth <= kMaxSplitK, tl.ws sized
@@ -144,36 +145,48 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
 
   // this lane's slot in its (chunk csel, k-half khalf) hi plane; block pb = tile row pb
   const char* const hb = lds + (csel * 4 + 2 * khalf) * HPLANE + l16 * 16;
-  // tap k of the range (fully unrolled over the longest range, so the weight buffers are
-  // compile-time registers -- a rolled loop carried them across its back-edge through copies that
-  // waited for every load): the weights of tap k + PF into buffer (k + PF) % (PF + 1), then tap
-  // k's MFMAs
-  // (a range holds NMAX - 1 or NMAX taps: 49 is not a multiple of 2, 3 or 4, so only the last
-  // step is conditional)
-  static_assert(KSQ % NTH != 0, "ranges of NMAX - 1 or NMAX taps");
-  const int n = t1 - t0;
-  constexpr int NMAX = (KSQ + NTH - 1) / NTH;
+  // one tap: the weights of tap t + PF into buffer (B + PF) % (PF + 1), then tap t's MFMAs from
+  // buffer B (B = the tap's index mod PF + 1, a compile-time constant)
+  auto step = [&](int t, auto bsel) {
+    constexpr int B = decltype(bsel)::value;
+    load_a(t + PF, abuf[(B + PF) % (PF + 1)]);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the step's start
+    const int tr = t / KS, tc = t - (t / KS) * KS;
+    const char* const tb = hb + (tr * PITCH + tc) * 16;
+    const AFrag& a = abuf[B];
 #pragma unroll
-  for (int k = 0; k < NMAX; ++k) {
-    if (k < NMAX - 1 || k < n) {
-      load_a(t0 + k + PF, abuf[(k + PF) % (PF + 1)]);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the step's start
-      const int t = t0 + k;
-      const int tr = t / KS, tc = t - (t / KS) * KS;
-      const char* const tb = hb + (tr * PITCH + tc) * 16;
-      const AFrag& a = abuf[k % (PF + 1)];
+    for (int pb = 0; pb < TR; ++pb) {
+      const bf16x8g bh = *(const bf16x8g*)(tb + pb * PITCH * 16);
+      const bf16x8g bl = *(const bf16x8g*)(tb + pb * PITCH * 16 + HPLANE);
 #pragma unroll
-      for (int pb = 0; pb < TR; ++pb) {
-        const bf16x8g bh = *(const bf16x8g*)(tb + pb * PITCH * 16);
-        const bf16x8g bl = *(const bf16x8g*)(tb + pb * PITCH * 16 + HPLANE);
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh, acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl, acc[cb][pb], 0, 0, 0);
-          acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh, acc[cb][pb], 0, 0, 0);
-        }
+      for (int cb = 0; cb < 2; ++cb) {
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh, acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bl, acc[cb][pb], 0, 0, 0);
+        acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh, acc[cb][pb], 0, 0, 0);
       }
     }
+  };
+  // A rolled loop of PF + 1 taps per iteration (each buffer index compile-time, so the back-edge
+  // carries the buffers in place), then the 0..PF remaining taps: 989 instead of 2248 lines of
+  // code with every tap unrolled, the same time (profiles/r05/ab_r05u_b1_m16q_rolled.log).
+  constexpr int G = PF + 1;
+  const int n = t1 - t0;
+  const int ng = n / G;
+  int t = t0;
+#pragma unroll 1
+  for (int i = 0; i < ng; ++i, t += G) {
+    step(t, std::integral_constant<int, 0>());
+    step(t + 1, std::integral_constant<int, 1>());
+    step(t + 2, std::integral_constant<int, 2>());
+    if constexpr (G > 3) step(t + 3, std::integral_constant<int, (G > 3 ? 3 : 0)>());
+    if constexpr (G > 4) step(t + 4, std::integral_constant<int, (G > 4 ? 4 : 0)>());
+  }
+  const int rem = n - ng * G;
+  if (rem > 0) step(t, std::integral_constant<int, 0>());
+  if (rem > 1) step(t + 1, std::integral_constant<int, 1>());
+  if constexpr (G > 3) {
+    if (rem > 2) step(t + 2, std::integral_constant<int, 2>());
+    if (rem > 3) step(t + 3, std::integral_constant<int, (G > 3 ? 3 : 0)>());
   }
 
 #if M16Q_STAMPS
