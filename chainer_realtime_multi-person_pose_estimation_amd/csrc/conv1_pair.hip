@@ -158,6 +158,9 @@ __global__ __launch_bounds__(256, 2) void conv1_pair_bf16x3(const uint8_t* __res
           a11l[cb][j] = (__bf16)(v - (float)h);
         }
       }
+#ifdef C1P_PROBE_NO11  // timing probe only (wrong results): conv1_1 skipped, the planes keep stale data
+      if (false)
+#endif
       for (int blk = wave; blk < (kP1Slots + 15) / 16; blk += 4) {
         const int sl = blk * 16 + l16;  // window slot = halo slot (row-major, pitch kP1HC)
         const int slc = min(sl, kP1Slots - 1);
