@@ -33,5 +33,7 @@ for v in variants:
     c3 = sorted(x[1]["conv3x3"] for x in out[v])
     c7 = sorted(x[1]["conv7x7"] for x in out[v])
     mr = sorted(x[1].get("map_resize", 0.0) for x in out[v])
-    print("%-8s fps median %.1f | conv3x3 median %.3f | conv7x7 median %.3f | map_resize median %.3f" %
-          (v, vals[len(vals) // 2], c3[len(c3) // 2], c7[len(c7) // 2], mr[len(mr) // 2]))
+    pp = sorted(x[1].get("postprocess", 0.0) for x in out[v])
+    print("%-8s fps median %.1f | conv3x3 median %.3f | conv7x7 median %.3f | map_resize median %.3f | "
+          "postprocess median %.3f" % (v, vals[len(vals) // 2], c3[len(c3) // 2], c7[len(c7) // 2], mr[len(mr) // 2],
+                                       pp[len(pp) // 2]))
