@@ -920,7 +920,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
   if (s.ks == 7) {
     if (!c128) return OP_OK;
     {
-      const int rc = launch_conv_m16q(s, g, cop_max, st, taken);
+      int rc = launch_conv_m16w(s, g, cop_max, st, taken);  // opt-in experiment (OP_M16W=1)
+      if (rc != OP_OK || *taken) return rc;
+      rc = launch_conv_m16q(s, g, cop_max, st, taken);
       if (rc != OP_OK || *taken) return rc;
     }
     if (raster_tiling(BigConfig{7, 5, 8, 128, 1, 1}, s.n, s.h, s.w, s.groups, cop_max, tl, true)) {
