@@ -520,6 +520,9 @@ __device__ __forceinline__ double rl_d(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+#ifndef GROUP_REG
+#define GROUP_REG 1
+#endif
 // grouping_key_points + subsets_to_pose_array, one wave per frame.
 // kBig: the subsets live in HBM (b.sub_ids / b.sub_sc, b.maxs rows, int32 peak ids) for any
 // peak and subset count; otherwise in LDS (<= kMaxSubsetsLds rows, int16 ids).
@@ -592,8 +595,21 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
   int nx_ia, nx_ib;
   double nx_sc;
   fetch(0, 0, nx_ia, nx_ib, nx_sc);
+  // Round 5 (GROUP_REG, LDS subsets): lane r < 64 also holds subset row r's ids at the current
+  // limb's two joints (cja, cjb) and its two scores (cs0, cs1) in registers, so the first 64 rows
+  // are matched without LDS reads and a matched row is updated by its own lane from registers; the
+  // LDS rows stay authoritative (every update writes through; merges and the final pass read them)
+  constexpr bool kReg = !kBig && GROUP_REG;
+  int cja = -1, cjb = -1;
+  double cs0 = 0.0, cs1 = 0.0;
   for (int l = 0; l < OP_N_LIMBS && status == OP_OK; ++l) {
     const int ja = s.limbs[l][0], jb = s.limbs[l][1];
+    if constexpr (kReg) {
+      if (lane < S) {
+        cja = ids[lane][ja];
+        cjb = ids[lane][jb];
+      }
+    }
     const int K = rl_i(kc, l);
     int my_ia = nx_ia, my_ib = nx_ib;
     double my_sc = nx_sc;
@@ -616,7 +632,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
       int found = 0, f0 = -1, f1 = -1;
       for (int s0 = 0; s0 < S; s0 += 64) {
         const int r = s0 + lane;
-        const bool m = r < S && (ids[r][ja] == ia || ids[r][jb] == ib);
+        const bool m = r < S && ((kReg && s0 == 0) ? (cja == ia || cjb == ib) : (ids[r][ja] == ia || ids[r][jb] == ib));
         unsigned long long bal = __ballot(m);
         while (bal) {
           const int k = __ffsll((long long)bal) - 1;
@@ -632,7 +648,16 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
         break;
       }
       if (found == 1) {
-        if (lane == 0 && ids[f0][jb] != ib) {
+        if (kReg && f0 < 64) {
+          if (lane == f0 && cjb != ib) {
+            ids[f0][jb] = (IdT)ib;
+            cjb = ib;
+            cs1 = __dadd_rn(cs1, 1.0);
+            cs0 = __dadd_rn(cs0, __dadd_rn(psb, score));
+            sc[f0][1] = cs1;
+            sc[f0][0] = cs0;
+          }
+        } else if (lane == 0 && ids[f0][jb] != ib) {
           ids[f0][jb] = (IdT)ib;
           sc[f0][1] = __dadd_rn(sc[f0][1], 1.0);
           sc[f0][0] = __dadd_rn(sc[f0][0], __dadd_rn(psb, score));
@@ -668,10 +693,40 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
             __syncthreads();
           }
           --S;
-        } else if (lane == 0) {
+          if constexpr (kReg) {  // rows f0 and past f1 changed: reload every lane's row
+            __syncthreads();
+            if (lane < S) {
+              cja = ids[lane][ja];
+              cjb = ids[lane][jb];
+              cs0 = sc[lane][0];
+              cs1 = sc[lane][1];
+            }
+          }
+        } else {
           const int fs[2] = {f0, f1};
           for (int q = 0; q < 2; ++q) {
             const int t = fs[q];
+            if (kReg && t < 64) {
+              if (lane == t) {
+                if (cja == -1) {
+                  ids[t][ja] = (IdT)ia;
+                  cja = ia;
+                  cs1 = __dadd_rn(cs1, 1.0);
+                  cs0 = __dadd_rn(cs0, __dadd_rn(psa, score));
+                  sc[t][1] = cs1;
+                  sc[t][0] = cs0;
+                } else if (cjb == -1) {
+                  ids[t][jb] = (IdT)ib;
+                  cjb = ib;
+                  cs1 = __dadd_rn(cs1, 1.0);
+                  cs0 = __dadd_rn(cs0, __dadd_rn(psb, score));
+                  sc[t][1] = cs1;
+                  sc[t][0] = cs0;
+                }
+              }
+              continue;
+            }
+            if (lane != 0) continue;
             if (ids[t][ja] == -1) {
               ids[t][ja] = (IdT)ia;
               sc[t][1] = __dadd_rn(sc[t][1], 1.0);
@@ -692,6 +747,12 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
         if (lane == 0) {
           sc[S][1] = 2.0;
           sc[S][0] = __dadd_rn(__dadd_rn(psa, psb), score);
+        }
+        if (kReg && lane == S) {
+          cja = ia;
+          cjb = ib;
+          cs1 = 2.0;
+          cs0 = __dadd_rn(__dadd_rn(psa, psb), score);
         }
         ++S;
       }
