@@ -112,20 +112,19 @@ MFMA_7X7 = {4: "v_mfma_f32_16x16x32_bf16", 5: "v_mfma_f32_16x16x32_bf16", 6: "v_
             8: "v_mfma_f32_16x16x32_bf16"}
 
 
-def committed_traffic(kernel, batch, precision, halo_mode):
-    """HBM bytes per launch (read + write) of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/**/*_traffic.json: FETCH_SIZE x 2 -- every fabric read request is 128 B and
-    FETCH_SIZE tallies it at 64 B, profiles/fetch_calib_r03.md -- + WRITE_SIZE,
-    tools/summarize_profile.py) taken on this exact workload; (None, None) when none matches."""
+def committed_traffic(kernel, workload, batch, precision, halo_mode, launch_ms=None):
+    """HBM bytes per launch (read + write) of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/**/*_traffic.json: FETCH_SIZE x 2 -- every fabric read request is 128 B and FETCH_SIZE
+    tallies it at 64 B, profiles/fetch_calib_r03.md -- + WRITE_SIZE, tools/summarize_profile.py)
+    taken on this exact workload (same workload string, batch, precision and 7x7 kernel family).
+    Among the matching sets: the newest round's, and within it the one whose average kernel time
+    is closest to this run's launch_ms (round-5 tags ranked by letter count
+    picked an older, slower set).  Returns (bytes, source, source_avg_ms), (None, None, None)
+    when none matches."""
     import glob
-    best = None
-    def age(q):  # tags r<round><letters>: r02ad follows r02z follows r02a
-        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(q))
-        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(q))
-
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")) +
-                   glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic.json")), key=age)
-    for p in paths:
+    cands = []
+    for p in glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")) + \
+            glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic.json")):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
@@ -133,12 +132,31 @@ def committed_traffic(kernel, batch, precision, halo_mode):
         cfg = d.get("config") or {}
         if cfg.get("frames_per_step_per_gpu") != batch or d.get("precision", "bf16x3") != precision:
             continue
+        if cfg.get("workload") and workload and cfg["workload"] != workload:
+            continue
         if KERNEL_7X7.get(d.get("halo_mode", 1)) != KERNEL_7X7.get(halo_mode):  # same 7x7 kernel
             continue
-        for k, v in d.get("kernels", {}).items():
-            if k.replace("op::", "").startswith(kernel):
-                best = (int(v["read_bytes"] + v["write_bytes"]), os.path.relpath(p, os.path.join(REPO, "profiles")))
-    return best if best else (None, None)
+        m = re.match(r"r(\d+)", os.path.basename(p))
+        rnd = int(m.group(1)) if m else -1
+        ks = {k.replace("op::", ""): v for k, v in d.get("kernels", {}).items()}
+        # every instantiation of the 7x7 family, weighted by its launches (sets from round 6 on record
+        # them): the roofline's launch_ms averages over all 7x7 launches too (C4 runs several tiles);
+        # older sets: the named instantiation alone
+        fam = [v for k, v in ks.items() if k.startswith(kernel.split(" ")[0]) and v.get("calls")]
+        if not fam:
+            fam = [dict(v, calls=1) for k, v in ks.items() if k.startswith(kernel)]
+        if not fam:
+            continue
+        calls = sum(v["calls"] for v in fam)
+        byts = sum((v["read_bytes"] + v["write_bytes"]) * v["calls"] for v in fam) / calls
+        avg_ms = sum(float(v.get("avg_ns", 0.0)) * v["calls"] for v in fam) / calls * 1e-6
+        dist = abs(avg_ms - launch_ms) / launch_ms if launch_ms and avg_ms > 0 else 0.0
+        cands.append(((rnd, -dist), int(byts), os.path.relpath(p, os.path.join(REPO, "profiles")),
+                      round(avg_ms, 4) or None))
+    if not cands:
+        return None, None, None
+    best = max(cands, key=lambda c: c[0])
+    return best[1], best[2], best[3]
 
 
 class Runner(object):
@@ -389,6 +407,10 @@ def bench_line(args, L, Wm, Fr, transport, rank, world, local):
     frames_total = world * B * args.steps
     value = frames_total / elapsed
     ms7, n7, fl7, by7 = prof["conv7x7"]
+    arith = "bf16x3: 3xBF16 split products, f32 accumulate" if args.precision == "bf16x3" else "exact f32 MFMA"
+    workload = ("%dx%d frames, full PoseDetector.%s path (upload, resize+normalise, 92-conv CocoPoseNet in %s, "
+                "PAF post-process), batch of %d frames per GPU per step"
+                % (FW, FH, "detect_precise" if args.precise else "__call__", arith, B))
     roofline = None
     if n7 > 0 and ms7 > 0:
         achieved = fl7 / (ms7 * 1e-3) / 1e12
@@ -411,16 +433,17 @@ def bench_line(args, L, Wm, Fr, transport, rank, world, local):
                 cen["npx"], key=cen["npx"].get)
         elif args.precision != "bf16x3" and cen["f32_lds"]:
             kern = "conv_f32_lds<7, 16> (7x7 stage convs, LDS halo, v_mfma_f32_32x32x2_f32)"
-        traffic, tsrc = committed_traffic(kern.split(" ")[0], B, args.precision, halo_mode)
+        traffic, tsrc, tsrc_ms = committed_traffic(kern.split(">")[0], workload, B, args.precision, halo_mode,
+                                                   ms7 / n7)
         roofline = {"bound": "mfma", "kernel": kern,
                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+                    "traffic_source_launch_ms": tsrc_ms,
                     "launch_ms": round(ms7 / n7, 4), "flops_per_launch": fl7 / n7,
                     "algorithmic_bytes_per_launch": by7 / n7}
     stage_ms = {k: round(v[0] / n_extra, 3) for k, v in prof_all.items()} if n_extra else {}
     metric = METRIC if headline else "frames/sec end-to-end (CNN+PAF grouping) at %dx%d%s, 1/2/4/8 MI355X" % (
         FW, FH, " multi-scale (%s)" % "/".join(str(v) for v in PARAMS_SCALES) if args.precise else "")
-    arith = "bf16x3: 3xBF16 split products, f32 accumulate" if args.precision == "bf16x3" else "exact f32 MFMA"
     maps_desc = ("post-process fed COCO-like %s maps from the reference's label generators%s" % (
         "6-person" if (FH, FW) == (368, 368) else "20-person",
         " (upsampled to the frame size: the full-resolution post-process)" if args.precise else "")
@@ -433,9 +456,7 @@ def bench_line(args, L, Wm, Fr, transport, rank, world, local):
         "data": "synthetic: seeded uint8 %dx%d BGR frames from a 2-batch pinned host pool, uploaded every step "
                 "inside the timed region (copy stream, overlapped with the previous step); random-init "
                 "CocoPoseNet (He-normal); %s" % (FW, FH, maps_desc),
-        "config": {"workload": "%dx%d frames, full PoseDetector.%s path (upload, resize+normalise, 92-conv "
-                               "CocoPoseNet in %s, PAF post-process), batch of %d frames per GPU per step"
-                               % (FW, FH, "detect_precise" if args.precise else "__call__", arith, B),
+        "config": {"workload": workload,
                    "frames_per_step_per_gpu": B, "net_input": "%dx%d" % (net_w, net_h),
                    "heatmap": "%dx%d" % optimal_size(FH, FW, 320) if not args.precise else "%dx%d" % (FW, FH),
                    "maps": args.maps, "parallelism": gather.label},

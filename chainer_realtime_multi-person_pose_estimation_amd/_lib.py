@@ -159,10 +159,37 @@ def lib():
 
 
 def build_info():
-    """The source digest baked into the loaded library at build time ("sha256:<hex>")."""
-    buf = ctypes.create_string_buffer(96)
+    """The provenance baked into the loaded library at build time: "sha256:<hex>;defs=<flags>" --
+    the digest of its sources and the build flags beyond csrc/Makefile's own (empty for the
+    product library)."""
+    buf = ctypes.create_string_buffer(1024)
     check(lib().op_build_info(buf, len(buf)), "op_build_info")
     return buf.value.decode("ascii")
+
+
+def build_digest():
+    """The source-digest part of build_info() ("sha256:<hex>")."""
+    return build_info().split(";", 1)[0]
+
+
+def build_flags():
+    """The build-flags part of build_info(): "" for the product library."""
+    info = build_info()
+    return info.split(";defs=", 1)[1] if ";defs=" in info else ""
+
+
+def check_provenance():
+    """Assert the loaded library is the product build of this tree: its source digest equals the
+    checked-out sources' and it was built without extra flags.  Returns the digest, or None when
+    the sources are absent (an install without csrc/: the digest cannot be verified, nor refuted)."""
+    flags = build_flags()
+    assert flags == "", "libopenpose_hip.so is an experiment build (flags %r): rebuild the product library" % flags
+    tree = source_digest()
+    if tree is None:
+        return None
+    built = build_digest()
+    assert built == tree, "libopenpose_hip.so digest %s != sources %s: rebuild it" % (built, tree)
+    return built
 
 
 def source_digest(csrc=None):

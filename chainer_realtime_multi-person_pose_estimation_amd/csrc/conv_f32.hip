@@ -28,9 +28,13 @@ __device__ __forceinline__ void dma16_f32(const void* gsrc, uint32_t lds_byte) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory");
 }
 
-// chunk boundary wait: every VMEM operation but the 4 youngest (the weight loads of the two steps
-// ahead, 2 per step) has completed -- i.e. this wave's halo pieces, issued before them
-__device__ __forceinline__ void wait_vmcnt_f32() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+// chunk boundary wait: every VMEM operation but the 2 * CB youngest (the weight loads of the two
+// steps ahead, CB per step) has completed -- i.e. this wave's halo pieces, issued before them
+template <int CB>
+__device__ __forceinline__ void wait_vmcnt_f32() {
+  static_assert(2 * CB <= 63, "vmcnt literal");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CB) : "memory");
+}
 
 template <int KS, int TCW>
 struct F32Tile {
@@ -135,7 +139,7 @@ __global__ __launch_bounds__(256, CB == 4 ? 2 : 1) void conv_f32_lds(ConvShape s
   auto boundary = [&](int it) {
     const int c = it / KSQ;
     if (it - c * KSQ != 0) return;
-    wait_vmcnt_f32();
+    wait_vmcnt_f32<CB>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (c + 1 < s.c8) issue_halo(c + 1, (c + 1) & 1);

@@ -259,13 +259,13 @@ struct KeepSlot {
   double* d_rows_view = nullptr;  // the device's address of h_rows (hipHostGetDevicePointer)
   int64_t h_rows_cap = 0;  // doubles
   int64_t rows_cap_now = 0;  // of them, usable by the current pack (OP_KEEP_ROWS_AVG)
-  int32_t* d_rows_cnt = nullptr;  // [0] h_rows allocator, [1] maps slots, [2] res slots
   PostRecord rec{};
   int n = 0;
   int grow = 0;  // overflow frames of the largest gather seen that needed a slot
 };
 constexpr int kKeepHdr = 5;  // int32 per frame in KeepSlot::d_hdr / h_hdr
 constexpr int64_t kKeepSlotBytes = 4ll << 30;  // keep-slot map bytes per gather slot (of 288 GB HBM)
+constexpr int64_t kKeepGrowBytes = 16ll << 30;  // ceiling of the grown slots' map bytes per gather slot
 
 enum BufId {
   B_X0, B_C11, B_C12, B_P1, B_C21, B_C22, B_P2, B_C3A, B_C3B, B_C34, B_P3, B_C41, B_C42, B_C43, B_CAT, B_BRA, B_BRB,
@@ -551,6 +551,7 @@ static int grow_buffer(op_ctx* c, void** p, size_t* cap, size_t bytes, const cha
     OP_HIP_CHECK(hipFree(*p));
   }
   *p = nullptr;
+  *cap = 0;  // a failed allocation below leaves no buffer, and says so
   OP_HIP_CHECK(hipMalloc(p, bytes + g_guard));
   *cap = bytes;
   guard_add(name, (char*)*p + bytes, nullptr);
@@ -1403,7 +1404,6 @@ int op_destroy(op_ctx* c) {
   if (c->up_pinned) hipHostFree(c->up_pinned);
   for (auto& k : c->keep) {
     if (k.h_rows) hipHostFree(k.h_rows);
-    if (k.d_rows_cnt) hipFree(k.d_rows_cnt);
     if (k.maps) hipFree(k.maps);
     if (k.res) hipFree(k.res);
     if (k.cnt) hipFree(k.cnt);
@@ -2321,11 +2321,9 @@ int op_fetch_maps(op_ctx* c, int32_t first, int32_t n, float* pafs, float* heatm
 // Record of frame i: int32 {status, n_peaks, n_persons, 0}, int64 global frame id, 8 pad bytes,
 // then max_persons x 54 f64 poses and max_persons f64 scores (rows past n_persons zero).
 __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, int max_persons, int64_t frame_base,
-                                                    int frame_stride, char* __restrict__ out, int64_t rec_bytes,
-                                                    int32_t* __restrict__ rows_cnt) {
+                                                    int frame_stride, char* __restrict__ out, int64_t rec_bytes) {
   const int i = blockIdx.x;
   const int f = first + i;
-  if (rows_cnt && i == 0 && threadIdx.x < 3) rows_cnt[threadIdx.x] = 0;  // keep_overflow's allocators
   char* r = out + (int64_t)i * rec_bytes;
   const int status = b.res_hdr[4 * f];
   const int persons = status == OP_OK ? b.res_hdr[4 * f + 2] : 0;
@@ -2348,45 +2346,98 @@ __global__ __launch_bounds__(256) void pack_records(PostBuffers b, int first, in
 
 int64_t record_bytes(int max_persons) { return 32 + (int64_t)max_persons * 55 * 8; }
 
-// Keep slot fill (see KeepSlot): per frame, its header and why its record cannot carry the whole
-// result.  A frame over the batched caps keeps its post-process input and batched peak counts (it
-// is re-run alone in big mode); a frame with more persons than the record holds keeps its batched
-// result rows (they are complete: copied out as they are).
-__global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, int max_persons, const float* __restrict__ src,
+// Keep slot plan (see KeepSlot; round 6): one block assigns every frame's keep
+// entry in FRAME ORDER -- exclusive prefix counts over the frames before it -- so which frame goes
+// without a slot when slots run short is always the same one (the last ones), whatever the block
+// scheduling (the per-block atomic claims it replaces were first come, first served).  Per frame:
+// why 2 (more persons than the record holds) takes page-locked rows while the rows of every earlier
+// why-2 frame plus its own fit h_rows_cap, else a device res slot; why 1 (over the batched caps) a
+// maps slot; a frame past `slots` such frames is not kept (where -1).
+__global__ __launch_bounds__(1024) void keep_plan(PostBuffers b, int first, int n, int max_persons, int have_src,
+                                                  int32_t* __restrict__ hdr, int64_t h_rows_cap, int slots) {
+  __shared__ int64_t s_rows[1024];
+  __shared__ int s_res[1024], s_map[1024];
+  __shared__ int64_t c_rows;
+  __shared__ int c_res, c_map;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    c_rows = 0;
+    c_res = 0;
+    c_map = 0;
+  }
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + t;
+    int status = 0, persons = 0, why = 0;
+    if (i < n) {
+      const int f = first + i;
+      status = b.res_hdr[4 * f];
+      persons = b.res_hdr[4 * f + 2];
+      why = status == OP_ERR_CAPACITY ? 1 : (status == OP_OK && persons > max_persons) ? 2 : 0;
+    }
+    const int64_t rows = why == 2 ? (int64_t)persons * 55 : 0;
+    __syncthreads();  // the carries of the previous chunk are visible, its scans are consumed
+    const int64_t r0 = c_rows;
+    s_rows[t] = rows;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // inclusive scan of the rows
+      const int64_t v = t >= d ? s_rows[t - d] : 0;
+      __syncthreads();
+      s_rows[t] += v;
+      __syncthreads();
+    }
+    const int64_t o = r0 + s_rows[t] - rows;  // doubles of h_rows before this frame's
+    const bool in_rows = why == 2 && o + rows <= h_rows_cap;
+    const int need_res = why == 2 && !in_rows, need_map = why == 1 && have_src;
+    s_res[t] = need_res;
+    s_map[t] = need_map;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int vr = t >= d ? s_res[t - d] : 0, vm = t >= d ? s_map[t - d] : 0;
+      __syncthreads();
+      s_res[t] += vr;
+      s_map[t] += vm;
+      __syncthreads();
+    }
+    if (i < n) {
+      int off = -1;
+      if (in_rows) off = (int)o;
+      else if (need_res) {
+        const int sl = c_res + s_res[t] - 1;
+        if (sl < slots) off = -2 - sl;
+      } else if (need_map) {
+        const int sl = c_map + s_map[t] - 1;
+        if (sl < slots) off = sl;
+      }
+      int32_t* h = hdr + kKeepHdr * i;
+      h[0] = status;
+      h[1] = b.res_hdr[4 * (first + i) + 1];
+      h[2] = status == OP_OK ? persons : 0;
+      h[3] = why;
+      h[4] = off;
+    }
+    __syncthreads();
+    if (t == 1023) {
+      c_rows = r0 + s_rows[1023];
+      c_res += s_res[1023];
+      c_map += s_map[1023];
+    }
+  }
+}
+
+// Keep slot fill: per frame, as keep_plan assigned it.  A frame over the batched caps keeps its
+// post-process input and batched peak counts (it is re-run alone in big mode); a frame with more
+// persons than the record holds keeps its batched result rows (they are complete: copied out as
+// they are).
+__global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, const float* __restrict__ src,
                                                      int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
-                                                     double* __restrict__ res, int32_t* __restrict__ hdr,
-                                                     double* __restrict__ h_rows, int64_t h_rows_cap,
-                                                     int32_t* __restrict__ rows_cnt, int slots) {
+                                                     double* __restrict__ res, const int32_t* __restrict__ hdr,
+                                                     double* __restrict__ h_rows) {
   const int i = blockIdx.x;
   const int f = first + i;
-  const int status = b.res_hdr[4 * f];
-  const int persons = b.res_hdr[4 * f + 2];
-  const int why = status == OP_ERR_CAPACITY ? 1 : (status == OP_OK && persons > max_persons) ? 2 : 0;
-  __shared__ int off_s;
-  if (threadIdx.x == 0) {
-    int off = -1;
-    if (why == 2) {  // rows -> page-locked host memory, if the slot's capacity holds them, else a res slot
-      const int o = atomicAdd(rows_cnt, persons * 55);
-      if ((int64_t)o + persons * 55 <= h_rows_cap) off = o;
-      else {
-        const int sl = atomicAdd(rows_cnt + 2, 1);
-        if (sl < slots) off = -2 - sl;
-      }
-    } else if (why == 1 && src) {
-      const int sl = atomicAdd(rows_cnt + 1, 1);
-      if (sl < slots) off = sl;
-    }
-    off_s = off;
-    hdr[kKeepHdr * i] = status;
-    hdr[kKeepHdr * i + 1] = b.res_hdr[4 * f + 1];
-    hdr[kKeepHdr * i + 2] = status == OP_OK ? persons : 0;
-    hdr[kKeepHdr * i + 3] = why;
-    hdr[kKeepHdr * i + 4] = off;
-  }
-  __syncthreads();
-  const int off = off_s;
+  const int why = hdr[kKeepHdr * i + 3], off = hdr[kKeepHdr * i + 4];
   if (why == 2) {
     if (off == -1) return;
+    const int persons = hdr[kKeepHdr * i + 2];
     const double* ps = b.res_poses + (int64_t)f * b.maxs * 54;
     const double* ss = b.res_scores + (int64_t)f * b.maxs;
     double* d = off >= 0 ? h_rows + off : res + (int64_t)(-2 - off) * b.maxs * 55;
@@ -2411,10 +2462,8 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     set_error("pack records: bad frame range");
     return OP_ERR_INVALID;
   }
-  int32_t* rows_cnt = nullptr;
   if (keep_slot >= 0) {
     KeepSlot& k = c->keep[keep_slot];
-    if (!k.d_rows_cnt) OP_HIP_CHECK(hipMalloc((void**)&k.d_rows_cnt, 3 * sizeof(int32_t)));
     // page-locked rows for frames past max_persons: 256 persons per frame on average (the rest,
     // if ever, are read from the device copy in res; OP_KEEP_ROWS_AVG overrides the 256, 0 sends
     // every such frame through the device copy -- a test aid)
@@ -2433,11 +2482,10 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.h_rows_cap = want;
       k.rows_cap_now = want;
     }
-    rows_cnt = k.d_rows_cnt;
   }
   RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
     hipLaunchKernelGGL(pack_records, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, frame_base,
-                       frame_stride, (char*)dst, record_bytes(max_persons), rows_cnt);
+                       frame_stride, (char*)dst, record_bytes(max_persons));
     OP_AFTER_LAUNCH("pack_records", c->stream);
     return OP_OK;
   }));
@@ -2447,20 +2495,39 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
     const float* src = r.kind == 1 ? r.low.base : r.kind == 2 ? r.full : nullptr;
     const int64_t fstride = r.kind == 1 ? r.low.fstride : r.fstride;
     const char* kf_env = getenv("OP_KEEP_FRAMES");
+    const int64_t per = src ? std::max<int64_t>(1, fstride * 4) : 1;  // map bytes per kept frame
+    int fit = n;  // the budget-sized count
     if (kf_env) {
       k.slots = std::min(n, std::max(1, atoi(kf_env)));
+      fit = k.slots;
     } else {
       const char* kb_env = getenv("OP_KEEP_BYTES");  // test aid: the map-byte budget per gather slot
       const int64_t budget = kb_env ? std::max(0ll, atoll(kb_env)) : kKeepSlotBytes;
-      const int64_t per = src ? std::max<int64_t>(1, fstride * 4) : 1;
-      const int64_t fit = std::max<int64_t>(8, budget / per);
-      k.slots = (int)std::min<int64_t>(n, std::max<int64_t>(fit, std::max(c->keep[0].grow, c->keep[1].grow)));
+      fit = (int)std::min<int64_t>(n, std::max<int64_t>(8, budget / per));
+      // a short gather grows the next packs' slots (`grow`), but never past kKeepGrowBytes of maps
+      // (advisor r05: growth was unbounded; one gather with many over-cap frames sized every later
+      // pack's slots for good, and a failed allocation then failed the pack instead of losing frames)
+      const char* kg_env = getenv("OP_KEEP_GROW_BYTES");  // test aid: the growth ceiling
+      const int64_t ceiling = kg_env ? std::max(0ll, atoll(kg_env)) : kKeepGrowBytes;
+      const int64_t grown = std::min<int64_t>(std::max(c->keep[0].grow, c->keep[1].grow),
+                                              std::max<int64_t>(8, ceiling / per));
+      k.slots = (int)std::min<int64_t>(n, std::max<int64_t>(fit, grown));
     }
-    if (src) {
-      RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)k.slots * fstride * 4, "keep_maps"));
-      RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)k.slots * OP_N_JOINTS * 4, "keep_cnt"));
+    // the slots' buffers; if the grown count cannot be allocated, fall back to the budget-sized one:
+    // the frames beyond it travel as lost-frame statuses rather than failing the pack
+    auto alloc = [&]() -> int {
+      if (src) {
+        RC(grow_buffer(c, (void**)&k.maps, &k.maps_cap, (size_t)k.slots * fstride * 4, "keep_maps"));
+        RC(grow_buffer(c, (void**)&k.cnt, &k.cnt_cap, (size_t)k.slots * OP_N_JOINTS * 4, "keep_cnt"));
+      }
+      return grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)k.slots * c->pb.maxs * 55 * 8, "keep_res");
+    };
+    if (alloc() != OP_OK) {
+      if (k.slots <= fit) return OP_ERR_HIP;
+      (void)hipGetLastError();  // the failed hipMalloc's error: the smaller request below decides
+      k.slots = fit;
+      RC(alloc());
     }
-    RC(grow_buffer(c, (void**)&k.res, &k.res_cap, (size_t)k.slots * c->pb.maxs * 55 * 8, "keep_res"));
     k.maxs = c->pb.maxs;
     const size_t hb = (size_t)n * kKeepHdr * 4;
     if (hb > k.hdr_cap) {
@@ -2475,8 +2542,11 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.hdr_cap = hb;
     }
     RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
-      hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, max_persons, src, fstride,
-                         k.maps, k.cnt, k.res, k.d_hdr, k.d_rows_view, k.rows_cap_now, k.d_rows_cnt, k.slots);
+      hipLaunchKernelGGL(keep_plan, dim3(1), dim3(1024), 0, c->stream, c->pb, first, n, max_persons, src ? 1 : 0,
+                         k.d_hdr, k.rows_cap_now, k.slots);
+      OP_AFTER_LAUNCH("keep_plan", c->stream);
+      hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, src, fstride, k.maps, k.cnt,
+                         k.res, k.d_hdr, k.d_rows_view);
       OP_AFTER_LAUNCH("keep_overflow", c->stream);
       return OP_OK;
     }));

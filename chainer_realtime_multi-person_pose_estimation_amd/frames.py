@@ -336,10 +336,12 @@ class RcclGather(object):
                     cap = res.n_persons
                     continue
                 break
-            if rc == lib_.OP_ERR_CAPACITY:
+            if rc == lib_.OP_ERR_CAPACITY and res.status != lib_.OP_ERR_CAPACITY:
                 # no keep slot held this frame (more overflow frames than slots in one gather; the
                 # library grows the slots for the next packs): it travels as a frame status through
-                # the exchange below -- an exception here would leave the other ranks waiting in it
+                # the exchange below -- an exception here would leave the other ranks waiting in it.
+                # (A re-run whose own frame status is OP_ERR_CAPACITY is not a lost frame: its status
+                # travels below like any other -- advisor r05)
                 self.lost += 1
                 self.lost_msg = lib_.last_error()
                 out.append((base + int(i) * stride, STATUS_CAPACITY, int(res.n_peaks),

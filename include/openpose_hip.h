@@ -77,10 +77,12 @@ typedef struct op_ctx op_ctx;
 
 const char* op_last_error(void);
 
-/* Provenance of the loaded binary (no reference counterpart): writes "sha256:<64 hex>" + NUL into
- * out (cap >= 72), the digest of the library's sources as built -- sha256 of the `sha256sum`
- * listing of csrc/ *.hip *.hpp *.cpp, csrc/Makefile and include/ *.h (paths relative to csrc/, sorted),
- * computed by the Makefile at build time; _lib.source_digest() recomputes it from the tree. */
+/* Provenance of the loaded binary (no reference counterpart): writes "sha256:<64 hex>;defs=<flags>"
+ * + NUL into out (OP_ERR_INVALID when cap is too small), the digest of the library's sources as
+ * built -- sha256 of the `sha256sum` listing of csrc/ *.hip *.hpp *.cpp, csrc/Makefile and
+ * include/ *.h (paths relative to csrc/, sorted), computed by the Makefile at build time;
+ * _lib.source_digest() recomputes it from the tree -- and the build flags beyond the Makefile's own
+ * (DEFS, FLAGS_* overrides; empty for the product library). */
 int op_build_info(char* out, int32_t cap);
 int op_default_params(op_params* p);
 int op_default_limits(op_limits* l);

@@ -27,10 +27,36 @@ def test_loaded_library_is_built_from_this_tree(lib):
     compiled from (csrc/Makefile bakes it in); it must equal the digest of the checked-out csrc/ and
     include/ -- a stale or foreign binary fails here (and in smoke() on the GPU box)."""
     got = lib.build_info()
-    assert re.fullmatch(r"sha256:[0-9a-f]{64}", got), got
-    assert got == lib.source_digest(), "libopenpose_hip.so was not built from this tree's sources: rebuild it"
+    assert re.fullmatch(r"sha256:[0-9a-f]{64};defs=.*", got), got
+    # advisor r05: the build flags are part of the provenance; the product library has none
+    assert lib.build_flags() == "", "experiment build flags in the product library: %r" % lib.build_flags()
+    assert lib.build_digest() == lib.source_digest(), "libopenpose_hip.so was not built from this tree's sources: rebuild it"
+    assert lib.check_provenance() == lib.build_digest()
     buf = ctypes.create_string_buffer(8)
     assert lib.lib().op_build_info(buf, len(buf)) == lib.OP_ERR_INVALID  # too small: refused, nothing written
+
+
+def test_provenance_without_sources(lib, monkeypatch):
+    """advisor r05: with no csrc/ to hash (an install without sources) the digest is unverifiable:
+    check_provenance() reports None instead of failing on a mismatch."""
+    monkeypatch.setattr(lib, "source_digest", lambda csrc=None: None)
+    assert lib.check_provenance() is None
+
+
+def test_build_flags_reach_the_provenance(tmp_path):
+    """advisor r05: an experiment build's flags (DEFS) are baked into op_build_info, so a probe
+    library copied over the product one fails check_provenance(); build_info.cpp alone, compiled the
+    way the Makefile compiles it."""
+    import subprocess
+    src = os.path.join(REPO, PKG_NAME, "csrc", "build_info.cpp")
+    so = str(tmp_path / "bi.so")
+    subprocess.run(["g++", "-shared", "-fPIC", "-std=c++17", "-I", os.path.join(REPO, "include"),
+                    "-DOP_BUILD_DIGEST=\"%s\"" % ("0" * 64), "-DOP_BUILD_FLAGS=\"-DC1P_PROBE_NO11=1\"",
+                    src, "-o", so], check=True)
+    L = ctypes.CDLL(so)
+    buf = ctypes.create_string_buffer(256)
+    assert L.op_build_info(buf, len(buf)) == 0
+    assert buf.value.decode() == "sha256:" + "0" * 64 + ";defs=-DC1P_PROBE_NO11=1"
 
 
 def test_layer_table_matches_cocoposenet(lib):

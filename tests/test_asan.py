@@ -24,7 +24,7 @@ L = import_module("chainer_realtime_multi-person_pose_estimation_amd._lib")
 F = import_module("chainer_realtime_multi-person_pose_estimation_amd.frames")
 lib = L.lib()
 assert lib._name.endswith("libopenpose_hip.asan.so"), lib._name
-assert L.build_info() == L.source_digest()
+assert L.build_digest() == L.source_digest()
 p = L.OpParams(); assert lib.op_default_params(ctypes.byref(p)) == 0
 lim = L.OpLimits(); assert lib.op_default_limits(ctypes.byref(lim)) == 0
 assert lib.op_default_params(None) != 0 and lib.op_default_limits(None) != 0

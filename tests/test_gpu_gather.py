@@ -186,8 +186,9 @@ def test_keep_slots_are_bounded(ctx, monkeypatch):
         g.submit(0, n, 0, 1)
         raw, ovf = g.wait(raw=True)
         assert g.lost == 1 and "keep slots" in g.lost_msg, (g.lost, g.lost_msg)
-        # the slot goes to whichever frame's block claims it first: one kept whole, one reported lost
-        assert sorted(r[1] for r in ovf) == [0, F.STATUS_CAPACITY] and sorted(r[0] for r in ovf) == [0, 1], ovf
+        # slots are assigned in frame order (keep_plan): frame 0 is kept whole,
+        # frame 1 is the one reported lost -- on every run
+        assert [(r[0], r[1]) for r in sorted(ovf, key=lambda r: r[0])] == [(0, 0), (1, F.STATUS_CAPACITY)], ovf
         assert F.count_persons(raw, MAXP, ovf)[1] == 1
         monkeypatch.setenv("OP_KEEP_FRAMES", "2")  # read per pack: both frames kept again
         ctx.run_staged()
@@ -229,6 +230,8 @@ def test_keep_slots_grow_after_a_short_gather(fresh_ctx, monkeypatch):
         g.submit(0, n, 0, 1)
         raw, ovf = g.wait(raw=True)
         assert g.lost == 2 and F.count_persons(raw, MAXP, ovf)[1] == 2
+        # frame order: the last two frames are the ones without a slot
+        assert sorted(r[0] for r in ovf if r[1] == F.STATUS_CAPACITY) == [8, 9], ovf
         fresh_ctx.run_staged()
         g.submit(0, n, 0, 1)
         raw, ovf = g.wait(raw=True)
@@ -237,6 +240,36 @@ def test_keep_slots_grow_after_a_short_gather(fresh_ctx, monkeypatch):
         want = fresh_ctx.fetch_results(0, n)
         for r in ovf:
             assert np.array_equal(r[3], np.asarray(want[r[0]][0]).reshape(r[3].shape)), r[0]
+    finally:
+        fresh_ctx.use_staged_maps(False)
+        g.close()
+
+
+def test_keep_slot_growth_is_capped(fresh_ctx, monkeypatch):
+    """advisor r05: a short gather grows the next packs' keep slots, but only up to a byte ceiling
+    (16 GiB of maps per gather slot; OP_KEEP_GROW_BYTES, test aid, lowers it): with a budget of 1
+    byte and a 1-byte ceiling, 12 frames past max_persons get the minimum 8 slots in both gathers,
+    the same 4 frames (8-11, frame order) are reported lost both times, and the pack never fails."""
+    monkeypatch.setenv("OP_KEEP_ROWS_AVG", "0")
+    monkeypatch.setenv("OP_KEEP_BYTES", "1")
+    monkeypatch.setenv("OP_KEEP_GROW_BYTES", "1")
+    monkeypatch.delenv("OP_KEEP_FRAMES", raising=False)
+    F = pkg_module("frames")
+    six = load_golden("six_people")
+    six_maps = np.concatenate([six["paf_low"], six["heat_low"]])
+    n = 12
+    fresh_ctx.stage_frames(np.zeros((n, 368, 368, 3), np.uint8))
+    g = F.RcclGather(fresh_ctx, F.SocketTransport(0, 1), max_persons=MAXP, timeout=60)
+    try:
+        fresh_ctx.stage_maps(np.stack([six_maps] * n))
+        fresh_ctx.use_staged_maps(True)
+        for step in range(2):
+            fresh_ctx.run_staged()
+            g.submit(0, n, 0, 1)
+            raw, ovf = g.wait(raw=True)
+            assert g.lost == 4 * (step + 1), (step, g.lost)
+            assert sorted(r[0] for r in ovf if r[1] == F.STATUS_CAPACITY) == [8, 9, 10, 11], ovf
+            assert F.count_persons(raw, MAXP, ovf)[1] == 4
     finally:
         fresh_ctx.use_staged_maps(False)
         g.close()

@@ -70,7 +70,7 @@ def main():
         wr = 1024 * sum(w) / len(w) / 1e6 if w else None
         if fr is not None and wr is not None:
             traffic[short(name)] = {"read_bytes": fr * 1e6, "write_bytes": wr * 1e6, "avg_ns": float(r["AverageNs"]),
-                                   "fetch_factor": round(fetch_factor(name), 4)}
+                                   "calls": int(r["Calls"]), "fetch_factor": round(fetch_factor(name), 4)}
         lines.append("| `%s` | %s | %.1f | %.2f | %s | %s |" % (
             short(name)[:80], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["Percentage"]),
             "%.1f" % fr if fr is not None else "-", "%.1f" % wr if wr is not None else "-"))
