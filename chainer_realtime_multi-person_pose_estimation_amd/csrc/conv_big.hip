@@ -653,7 +653,12 @@ static bool raster_tiling(const BigConfig& k, int n, int h, int w, int groups, i
   const int budget = k.lds_budget() - k.ring_bytes();
   int tiles = 0, rows_max = 0, pitch = 0, nh = 0, fa = 0;
   bool ok = false;
-  for (int variant = 0; variant < (wide ? 4 : 1) && !ok; ++variant) {
+  // conv_m16 (wide): the tight pitch w + ks - 1 first (round 6: the headline's 7x7 75.6 -> 75.2 ms per
+  // step, profiles/r06/ab_r06a_tight_pitch_ring4.log -- the 16-B slots of a block that wraps a row
+  // see a few 2-way bank conflicts, but 22 instead of 27 KiB halo planes load and fit a circular
+  // second chunk, conv_m16.hip CIRC); OP_M16_TIGHT=0 (A/B aid) starts from w + 16
+  static const bool tight_first = !(getenv("OP_M16_TIGHT") && atoi(getenv("OP_M16_TIGHT")) == 0);
+  for (int variant = (wide && tight_first) ? 1 : 0; variant < (wide ? 4 : 1) && !ok; ++variant) {
     const bool aligned = variant >= 2;
     pitch = (variant & 1) ? w + k.ks - 1 : halo_pitch(w, k.ks);
     fa = aligned ? (hw + cap - 1) / cap : 0;

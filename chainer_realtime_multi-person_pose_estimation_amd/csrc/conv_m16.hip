@@ -10,6 +10,12 @@
 #ifndef M16_DMA_HALF
 #define M16_DMA_HALF 1
 #endif
+// taps of the staggered kernel's weight ring: 6 (three pair slots, 28-KiB halo planes) by default;
+// 4 (32-KiB planes) for A/Bs
+#ifndef M16_STAG_RING
+#define M16_STAG_RING 6
+#endif
+static_assert(M16_STAG_RING == 6 || M16_STAG_RING == 4, "staggered ring: 4 or 6 taps");
 
 namespace op {
 
@@ -48,22 +54,37 @@ __device__ unsigned long long g_m16_st[12];
 // planes (7x7 -1.8 %, profiles/r05/ab_r05l_*) than with the 4-tap ring (+1.4 %, ab_r05o_*), so it
 // takes that where nh <= 28 (the 46 x 46 batch rasters: 27); the deep 12-tap ring (small tiles:
 // one frame's split-K launches) is staggered as it is (one frame's 7x7 -4.7 %).
-template <int KS, int NPX, bool DEEP = false, bool STAG = false>
+// CIRC (round 6): no chunk-boundary drain for tiles of one frame.  Each halo
+// plane is a circular buffer of CP = HPLANE / 1 KiB pieces; chunk c's np pieces sit at physical
+// pieces cbase_c .. cbase_c + np - 1 (mod CP), chunk c + 1 right after them, and a B fragment's
+// slot is wrapped (one v_min_u32 per block) on its way into the LDS address.  Waves 4-7 (which
+// stage no weights) each stream one plane of chunk c + 1 in the background, one 1-KiB piece at a
+// time, in three regions: R1, the pieces that overlay no live data, during pairs 2-20 of chunk c;
+// R2, those overlaying chunk c's halo rows 0-5 (read only by taps with ky <= 5, i.e. pairs <= 20),
+// during pairs 21-22; R3, those overlaying chunk c's later rows, during pairs 0-1 of chunk c + 1 --
+// allowed only when R3 holds rows that chunk c + 1 first reads with ky >= 1 (pair 3 on).  A piece
+// issued by waves 4-7 at the start of pair p is waited for (vmcnt) at their start of pair p + 1 and
+// ordered by the ring barrier they meet in its middle, so every wave may read it from pair p + 2;
+// the staggered ring barriers then run on across chunk boundaries.  Tiles that cross a frame
+// border (two row sets, ~30 % at 640 px on 46 x 46 maps) or whose R3 would hold early rows keep
+// the drain.  Bit-identical: the same MFMAs on the same data in the same order.
+template <int KS, int NPX, bool DEEP = false, bool STAG = false, bool CIRC = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
   static_assert(!STAG || M16_DMA_HALF, "staggered halves: waves 4-7 must not stage the ring");
+  static_assert(!CIRC || (STAG && !DEEP && KS == 7), "circular halo: the staggered 7x7 ring kernel only");
   constexpr int KSQ = KS * KS;
   constexpr int R = KS / 2;
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
   constexpr int PLANE_W = CW * 16;
   constexpr int SLOT_W = 4 * PLANE_W;
-  constexpr int RING = DEEP ? 12 : (STAG ? 6 : 4);  // taps; even, so a pair never wraps
+  constexpr int RING = DEEP ? 12 : (STAG ? M16_STAG_RING : 4);  // taps; even, so a pair never wraps
   constexpr int AHEAD = DEEP ? 5 : 1;               // tap pairs staged ahead of the one being computed
   constexpr int CAP = PG * NPX * 16;
   // halo planes at a fixed stride (raster_tiling keeps nh <= 32; DEEP: nh <= 16; STAG: nh <= 28),
   // placed first so a lane's lo-plane read is its hi-plane address + an immediate offset; the
   // weight ring follows
-  constexpr int HPLANE = (DEEP ? 16 : (STAG ? 28 : 32)) * 1024;
+  constexpr int HPLANE = (DEEP ? 16 : (STAG ? (M16_STAG_RING == 6 ? 28 : 32) : 32)) * 1024;
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
 
   const int lin = blockIdx.x;
@@ -166,6 +187,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int h_plane = wave & 3, h_i0 = wave >> 2;
   const int h_sl0 = h_i0 * 64 + lane;
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
+  // CIRC: this lane's row / column in piece 0 of a plane (the background cursor's start)
+  const int hq_r0 = lane / tl.pitch, hq_c0 = lane - (lane / tl.pitch) * tl.pitch;
   // this wave's pieces of chunk c's halo (LDS-DMA)
   auto issue_halo = [&](int c, const Tile& T) {
     const char* const fbase = (const char*)g.in + (int64_t)T.frame * hp_in * wp_in * pix_bytes;
@@ -193,6 +216,28 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const unsigned long long st_t0 = M16_T();
 #endif
   const Tile T = tile_of(widx);
+  // CIRC schedule of this tile (wave-uniform): np pieces per chunk and its regions R1 / R2 / R3
+  constexpr int CP = HPLANE / 1024;
+  int c_np = 0, c_r1 = 0, c_r2 = 0, c_r3 = 0;
+  bool circ = false;
+  if constexpr (CIRC) {
+    if (T.fb == T.frame && cb1 - cb0 > 1) {
+      const int rows = (T.P1 - T.frame * tl.hw) / s.w - T.y0 + 1 + 2 * R;  // output rows + the 2R border
+      const int np = (rows * tl.pitch + 63) / 64;
+      const int op = max(2 * np - CP, 0);         // pieces of chunk c + 1 that overlay chunk c's
+      const int early = (6 * tl.pitch) / 64;      // chunk c's pieces inside its rows 0-5
+      c_np = np;
+      c_r2 = min(op, early);
+      c_r3 = op - c_r2;
+      c_r1 = np - op;
+      // R3's first row must be read by taps with ky >= 1 only: row >= the tile's output rows
+      circ = np <= CP && (c_r3 == 0 || ((np - c_r3) * 64) / tl.pitch >= rows - 2 * R);
+    }
+    c_np = __builtin_amdgcn_readfirstlane(c_np);
+    c_r1 = __builtin_amdgcn_readfirstlane(c_r1);
+    c_r2 = __builtin_amdgcn_readfirstlane(c_r2);
+    c_r3 = __builtin_amdgcn_readfirstlane(c_r3);
+  }
 #pragma unroll
   for (int j = 0; j < 2 * AHEAD; ++j) stage_w(cb0 * KSQP + j);
   {
@@ -208,8 +253,39 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
         const int y = pp / s.w, x = pp - (pp / s.w) * s.w;
         q = (f == T.frame ? y - T.y0 : T.rowsA + y) * tl.pitch + x;
       }
-      qb[pb] = (2 * khalf) * HPLANE + q * 16;
+      qb[pb] = CIRC ? q * 16 : (2 * khalf) * HPLANE + q * 16;  // CIRC: the plane base is added per read
     }
+    const int pbase = (2 * khalf) * HPLANE;  // CIRC: this lane's hi plane
+    // CIRC: a lane's byte offset of block pb's slot + the tap offset, wrapped into the plane
+    auto bofs = [&](int pb, int toff) -> int {
+      if constexpr (CIRC) {
+        const unsigned a = (unsigned)(qb[pb] + toff);
+        return (int)min(a, a - (unsigned)HPLANE) + pbase;
+      } else {
+        return qb[pb] + toff;
+      }
+    };
+    // CIRC: waves 4-7's background halo stream of plane wave - 4: pieces [jlo, jhi) of chunk cc into
+    // physical pieces base + j (mod CP); the cursor (hq_r, hq_c) is the lane's row / column of piece jlo
+    int hq_r = 0, hq_c = 0;
+    const int hq_pl = wave & 3;
+    auto circ_issue = [&](int cc, int jlo, int jhi, int base) {
+      const char* const src0 = (const char*)g.in + (int64_t)T.frame * hp_in * wp_in * pix_bytes +
+                               (int64_t)(cc * 4 + hq_pl) * in_pc;
+      for (int j = jlo; j < jhi; ++j) {
+        const int yy = min(T.y0 - R + hq_r + s.pin, hp_in - 1);
+        const int xx = min(hq_c - R + s.pin, wp_in - 1);
+        int ph = base + j;
+        ph = ph >= CP ? ph - CP : ph;
+        glds16((const void*)(src0 + (int64_t)(yy * wp_in + xx) * in_px), halo + hq_pl * HPLANE + ph * 1024);
+        hq_c += 64;
+        while (hq_c >= tl.pitch) {
+          hq_c -= tl.pitch;
+          ++hq_r;
+        }
+      }
+    };
+    int cbase = 0;  // CIRC: the current chunk's first physical piece
 
     floatx4 acc[4][NPX];
 #pragma unroll
@@ -228,16 +304,24 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       const unsigned long long tb0 = M16_T();
       __builtin_amdgcn_sched_barrier(0);
 #endif
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      // the chunk-boundary drain (CIRC tiles: only before their first chunk)
+      const bool cont = CIRC && circ && c > cb0;  // the ring barriers run on from the previous chunk
+      if (!cont) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
 #if M16_PROBE_NOHALO  // timing probe only (wrong results): the halo is loaded for the first chunk only
-      if (c == cb0) issue_halo(c, T);
+        if (c == cb0) issue_halo(c, T);
 #else
-      issue_halo(c, T);
+        issue_halo(c, T);
 #endif
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      int nbase = cbase + c_np;  // CIRC: the next chunk's first physical piece
+      nbase = nbase >= CP ? nbase - CP : nbase;
+      const bool has_next = c + 1 < cb1;
+      const bool cont_next = CIRC && circ;  // the next chunk continues without a drain
 #if M16_STAMPS
       __builtin_amdgcn_sched_barrier(0);
       st_b += M16_T() - tb0;
@@ -266,11 +350,11 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #if !M16_PROBE_NOBAR  // timing probe only (racy ring): no per-pair barrier
         if (!STAG) {
           __builtin_amdgcn_s_barrier();  // ... landed for every wave; the previous pair's slots are free
-        } else if (wave < 4 && t > 0) {
+        } else if (wave < 4 && (t > 0 || cont)) {
           // waves 0-3 at the start of pair p, waves 4-7 in the middle of pair p - 1 (below): pair p's
           // pieces landed for every wave; the slot staged next (pair p - 1's) is free -- waves 4-7
           // hold pair p - 1's A fragments in registers since they started it.  The chunk's first
-          // pair needs none: the chunk barriers above ordered everything
+          // pair needs none after a drain: the chunk barriers above ordered everything
           __builtin_amdgcn_s_barrier();
         }
 #endif
@@ -282,6 +366,31 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #endif
         stage_w(it + 2 * AHEAD);
         stage_w(it + 2 * AHEAD + 1);
+        if constexpr (CIRC) {
+          if (circ && wave >= 4) {  // the background halo stream (see CIRC above), pair p = t / 2
+            const int p = t >> 1;
+            int cc = c + 1, jlo = 0, jhi = 0, base = nbase;
+            if (p < 2) {  // R3 of this chunk, half per pair
+              const int j0 = c_np - c_r3, jm = j0 + (c_r3 + 1) / 2;
+              cc = c;
+              base = cbase;
+              jlo = p == 0 ? j0 : jm;
+              jhi = c > cb0 ? (p == 0 ? jm : c_np) : jlo;
+            } else if (p <= 20) {  // R1 of the next chunk over pairs 2-20
+              jlo = (p - 2) * c_r1 / 19;
+              jhi = has_next ? (p - 1) * c_r1 / 19 : jlo;
+            } else if (p <= 22) {  // R2 over pairs 21-22
+              const int jm = c_r1 + (c_r2 + 1) / 2;
+              jlo = p == 21 ? c_r1 : jm;
+              jhi = has_next ? (p == 21 ? jm : c_r1 + c_r2) : jlo;
+            }
+            if (p == 2) {
+              hq_r = hq_r0;
+              hq_c = hq_c0;
+            }
+            circ_issue(cc, jlo, jhi, base);
+          }
+        }
 #if M16_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const unsigned long long tp3 = M16_T();
@@ -303,19 +412,22 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
           al[cb] = *(const bf16x8g*)(wsl + PLANE_W + cb * 256);
         }
         bf16x8g bh[2], bl[2];
-        bh[0] = *(const bf16x8g*)(halo + qb[0] + toff);
-        bl[0] = *(const bf16x8g*)(halo + qb[0] + toff + HPLANE);
+        {
+          const char* bp = halo + bofs(0, toff);
+          bh[0] = *(const bf16x8g*)bp;
+          bl[0] = *(const bf16x8g*)(bp + HPLANE);
+        }
 #pragma unroll
         for (int pb = 0; pb < NPX; ++pb) {
           const int cur = pb & 1;
-          if (STAG && pb == NPX / 2 && wave >= 4 && t + 2 < kPairsEnd) {
+          if (STAG && pb == NPX / 2 && wave >= 4 && (t + 2 < kPairsEnd || (cont_next && has_next))) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();  // waves 0-3's barrier at the start of pair p + 1 (above)
             asm volatile("" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
           }
           if (pb + 1 < NPX) {
-            const char* bp = halo + qb[pb + 1] + toff;
+            const char* bp = halo + bofs(pb + 1, toff);
             bh[cur ^ 1] = *(const bf16x8g*)bp;
             bl[cur ^ 1] = *(const bf16x8g*)(bp + HPLANE);
           }
@@ -332,6 +444,16 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #endif
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[cb], bl[cur], acc[cb][pb], 0, 0, 0);
             acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[cb], bh[cur], acc[cb][pb], 0, 0, 0);
+          }
+        }
+      }
+      if constexpr (CIRC) {
+        if (circ) {  // the next chunk's pieces start where this chunk's end: move every block's slot
+          cbase = nbase;
+#pragma unroll
+          for (int pb = 0; pb < NPX; ++pb) {
+            const unsigned a = (unsigned)(qb[pb] + c_np * 1024);
+            qb[pb] = (int)min(a, a - (unsigned)HPLANE);
           }
         }
       }
@@ -425,7 +547,12 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 4, false, true>, (const void*)conv_m16_bf16x3<7, 3, false, true>,
                          (const void*)conv_m16_bf16x3<7, 2, false, true>,
                          (const void*)conv_m16_bf16x3<7, 5, true, true>, (const void*)conv_m16_bf16x3<7, 4, true, true>,
-                         (const void*)conv_m16_bf16x3<7, 3, true, true>, (const void*)conv_m16_bf16x3<7, 2, true, true>};
+                         (const void*)conv_m16_bf16x3<7, 3, true, true>, (const void*)conv_m16_bf16x3<7, 2, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 9, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 7, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -442,21 +569,29 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   const char* stag_env = getenv("OP_M16_STAG");
   // not on frame-aligned raster tiles (the wide multi-scale maps): C4's 7x7 79.2 ms staggered
   // everywhere, 78.5 never, 77.8 except those (profiles/r05/ab_r05p_7x7_stag_c4_modes.log)
-  const bool stag = M16_DMA_HALF && (deep || tl.nh <= 28) && tl.fa_tiles == 0 && !(stag_env && atoi(stag_env) == 0);
+  const bool stag = M16_DMA_HALF && (deep || tl.nh <= (M16_STAG_RING == 6 ? 28 : 32)) && tl.fa_tiles == 0 &&
+                    !(stag_env && atoi(stag_env) == 0);
   const int lds = deep ? 12 * 4 * 128 * 16 + 4 * 16 * 1024   // ring + 4 halo planes (16-KiB stride)
-                  : stag ? 6 * 4 * 128 * 16 + 4 * 28 * 1024  // 6-tap ring + 4 planes (28-KiB stride)
+                  : stag ? (M16_STAG_RING == 6 ? 6 * 4 * 128 * 16 + 4 * 28 * 1024  // 6-tap ring + 4 planes (28-KiB stride)
+                                               : 4 * 4 * 128 * 16 + 4 * 32 * 1024)
                          : 4 * 4 * 128 * 16 + 4 * 32 * 1024;  // ring + 4 halo planes (32-KiB stride)
   const unsigned blocks = tl.xpu ? 8u * (unsigned)((tl.per_unit + tl.xpu - 1) / tl.xpu * std::max(tl.pair, 1))
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
+  // round 6: the staggered kernel with circular halo planes (no chunk-boundary drain for tiles of
+  // one frame); OP_M16_CIRC=0 keeps the drain everywhere (A/B aid, read per call)
+  const char* circ_env = getenv("OP_M16_CIRC");
+  const bool circ = stag && !deep && npx >= 6 && !(circ_env && atoi(circ_env) == 0);
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
+#define M16_LAUNCH_C(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_CASE(N)                                  \
   case N:                                            \
     if (deep && N <= 5) {                            \
       if (stag) M16_LAUNCH(N, (N <= 5), true);       \
       else M16_LAUNCH(N, (N <= 5), false);           \
     } else if (stag) {                               \
-      M16_LAUNCH(N, false, true);                    \
+      if (circ && N >= 6) M16_LAUNCH_C((N >= 6 ? N : 6)); \
+      else M16_LAUNCH(N, false, true);               \
     } else {                                         \
       M16_LAUNCH(N, false, false);                   \
     }                                                \
@@ -471,12 +606,15 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
     M16_CASE(3)
     M16_CASE(2)
     default:
-      if (stag) M16_LAUNCH(10, false, true);
+      if (circ) M16_LAUNCH_C(10);
+      else if (stag) M16_LAUNCH(10, false, true);
       else M16_LAUNCH(10, false, false);
   }
 #undef M16_CASE
 #undef M16_LAUNCH
+#undef M16_LAUNCH_C
   census_add(stag ? OP_CENSUS_7X7_STAG : OP_CENSUS_7X7_PLAIN_RING);
+  if (circ) census_add(OP_CENSUS_7X7_CIRC);
 #if M16_STAMPS
   static const bool dump = getenv("OP_M16_STAMPS") != nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

@@ -312,6 +312,7 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_7X7_STAG 30       /* conv_m16 7x7 launches with the staggered halves (round 5) */
 #define OP_CENSUS_7X7_PLAIN_RING 31 /* ... with one ring barrier per pair for all 8 waves */
 #define OP_CENSUS_7X7_Q 32          /* 7x7 launches on the small-launch kernel conv_m16q_bf16x3 (round 5) */
+#define OP_CENSUS_7X7_CIRC 33       /* staggered conv_m16 7x7 launches with circular halo planes (round 6) */
 #define OP_CENSUS_SLOTS 40
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

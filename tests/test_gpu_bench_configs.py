@@ -322,6 +322,29 @@ def test_staggered_halves_bit_identical(lib, bctx, monkeypatch, n):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
 
 
+@pytest.mark.parametrize("n", [38, 232])
+def test_circular_halo_bit_identical(lib, bctx, monkeypatch, n):
+    """Round 6: the staggered 7x7 kernel with circular halo planes (conv_m16.hip CIRC: tiles of one
+    frame stream the next chunk's halo in the background instead of draining at every chunk
+    boundary; OP_M16_CIRC=0 keeps the drain) changes where a chunk's halo sits in LDS and when it is
+    loaded, not what any MFMA reads: the maps are bit-identical to the drained kernel at 38 frames
+    and at the headline's 232, and the census shows the circular kernel ran every 7x7 launch."""
+    rng = np.random.default_rng(700 + n)
+    x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
+    out = {}
+    for circ in ("1", "0"):
+        monkeypatch.setenv("OP_M16_CIRC", circ)
+        _census_npx(lib)
+        out[circ] = bctx.forward(x)
+        cen = _census_npx(lib)
+        print("n %d OP_M16_CIRC=%s census:" % (n, circ), cen)
+        assert cen["7x7_stag"] == 25, cen
+        assert cen["7x7_circ"] == (25 if circ == "1" else 0), cen
+    monkeypatch.delenv("OP_M16_CIRC")
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
 def test_staggered_halves_precise_720p(lib, monkeypatch):
     """The staggered 7x7 halves on the multi-scale path's wide maps (41- to 164-column maps, halo
     planes up to 32 KiB, frame-aligned and tight-pitch raster tiles): 2 frames of 1280x720 through
@@ -333,8 +356,9 @@ def test_staggered_halves_precise_720p(lib, monkeypatch):
     try:
         c.set_weights(_weights(case_weights("posenet", 0)))
         out = {}
-        for stag in ("1", "0"):
-            monkeypatch.setenv("OP_M16_STAG", stag)
+        for stag in ("1", "0", "circ0"):  # circ0: staggered, the circular halo off (round 6)
+            monkeypatch.setenv("OP_M16_STAG", "1" if stag == "circ0" else stag)
+            monkeypatch.setenv("OP_M16_CIRC", "0" if stag == "circ0" else "1")
             c.stage_frames(frames)
             _census_npx(lib)
             try:
@@ -344,12 +368,16 @@ def test_staggered_halves_precise_720p(lib, monkeypatch):
             c.synchronize()
             cen = _census_npx(lib)
             if stag == "1":  # the launches whose halo planes fit 28 KiB (and every deep-ring launch)
-                assert cen["7x7_stag"] > 0, cen
+                assert cen["7x7_stag"] > 0 and cen["7x7_circ"] > 0, cen
+            elif stag == "circ0":
+                assert cen["7x7_stag"] > 0 and cen["7x7_circ"] == 0, cen
             else:
                 assert cen["7x7_stag"] == 0 and cen["7x7_plain_ring"] == 4 * 25, cen
             out[stag] = c.fetch_maps(0, 2)
         monkeypatch.delenv("OP_M16_STAG")
-        for a, b in zip(out["1"], out["0"]):
-            assert np.array_equal(a, b), float(np.abs(a - b).max())
+        monkeypatch.delenv("OP_M16_CIRC")
+        for other in ("0", "circ0"):
+            for a, b in zip(out["1"], out[other]):
+                assert np.array_equal(a, b), (other, float(np.abs(a - b).max()))
     finally:
         c.close()

@@ -11,6 +11,8 @@
 #   c4prof             rocprofv3 kernel-trace stats of the C4 line
 #   evidence           tools/gpu_evidence.sh (kernel stats, FETCH/WRITE, SQ, clock passes)
 #   tcc                tools/gpu_tcc_bytes.sh (fabric reads by request size)
+#   prof:NAME[:ARGS]   tools/profile.sh NAME ARGS (kernel stats + FETCH/WRITE passes of one bench line,
+#                      e.g. prof:r06a_c5_m4_b64:--frame,720x1280 -> gpurun_out/prof_NAME)
 #   ablib:ARGS         tools/ab_lib.py ARGS (interleaved A/B of library variants; commas for spaces)
 #   abenv:TAG:A:B[:N]  tools/gpu_ab_env.sh (interleaved A/B of env settings on the default bench)
 #   abb1:TAG:A:B[:N]   tools/gpu_ab_b1.sh (the same on the one-frame line)
@@ -39,6 +41,8 @@ for step in "$@"; do
              --no-variants --no-profile) > $log 2>&1 ;;
     evidence) bash tools/gpu_evidence.sh $TAG > $log 2>&1 ;;
     tcc) bash tools/gpu_tcc_bytes.sh $TAG > $log 2>&1 ;;
+    prof) nm=${arg%%:*}; pa=${arg#*:}; [ "$pa" = "$arg" ] && pa=""
+          bash tools/profile.sh $nm ${pa//,/ } > $log 2>&1 ;;
     ablib) timeout -k 10 1100 python3 -u tools/ab_lib.py ${arg//,/ } > $log 2>&1 ;;
     abenv) IFS=: read -r t a b r <<< "$arg"; bash tools/gpu_ab_env.sh $t "$a" "$b" ${r:-2} > $log 2>&1 ;;
     abb1) IFS=: read -r t a b r <<< "$arg"; bash tools/gpu_ab_b1.sh $t "$a" "$b" ${r:-3} > $log 2>&1 ;;
