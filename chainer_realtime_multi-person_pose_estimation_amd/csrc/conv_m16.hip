@@ -579,9 +579,13 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                                  : (unsigned)(tl.units * tl.per_unit);
   const dim3 grid(blocks, (unsigned)tl.ksplit);
   // round 6: the staggered kernel with circular halo planes (no chunk-boundary drain for tiles of
-  // one frame); OP_M16_CIRC=0 keeps the drain everywhere (A/B aid, read per call)
+  // one frame) -- bit-identical, measured SLOWER and opt-in (OP_M16_CIRC=1, read per call): the 7x7
+  // class 77.2 -> 79.8 ms per headline step, and 79.6 with the circular kernel's drain on every tile
+  // (profiles/r06/ab_r06b_*): the pair loop is that sensitive to added per-pair instructions (its
+  // per-block slot wrap and the background schedule); so is it to fewer scalar but more vector ones
+  // (incremental staging cursor: 76.0 -> 80.4 ms, profiles/r06/ab_r06c_incr_scalar_cursor_not_kept.log)
   const char* circ_env = getenv("OP_M16_CIRC");
-  const bool circ = stag && !deep && npx >= 6 && !(circ_env && atoi(circ_env) == 0);
+  const bool circ = stag && !deep && npx >= 6 && circ_env && atoi(circ_env) == 1;
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_LAUNCH_C(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_CASE(N)                                  \
