@@ -880,6 +880,12 @@ static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, in
   const int pfk = tr == 4 && pf == 4 ? 4 : 2;
   while (nth > 2 && ncp * nth > kMaxSplitK) --nth;
   if (ncp * nth > kMaxSplitK) return OP_OK;
+  // round 6, opt-in (OP_M16Q_IWG=1): the 2 tap ranges of a chunk pair in one 8-wave workgroup,
+  // summed in LDS, so split K = the chunk pairs and the reduce reads half the partials -- measured
+  // slower: one frame's 7x7 class 0.95 -> 0.99 ms (profiles/r06/ab_r06g_b1_m16q_iwg_not_kept.log),
+  // the 8-wave workgroups' exchange and barrier cost more than the halved partial traffic saves
+  const char* iwg_env = getenv("OP_M16Q_IWG");
+  const bool iwg = tr == 4 && nth == 2 && pfk == 2 && iwg_env && atoi(iwg_env) == 1;
   BigTiling t{};
   t.tr = tr;
   t.tc = 16;
@@ -890,7 +896,7 @@ static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, in
   t.per_unit = s.n * t.tiles_y * t.tiles_x;
   t.hw = s.h * s.w;
   t.total = s.n * t.hw;
-  t.ksplit = ncp * nth;
+  t.ksplit = iwg ? ncp : ncp * nth;
   float* ws = splitk_ws(st, (size_t)t.ksplit * s.groups * t.total * cop_max);
   if (!ws) return OP_OK;  // capturing with a short workspace: conv_m16 unsplit now, re-captured later
   t.ws = ws;
@@ -899,7 +905,8 @@ static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, in
   census_add(OP_CENSUS_7X7_SPLITK);
   if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
-  const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t);
+  if (iwg) census_add(OP_CENSUS_7X7_Q_IWG);
+  const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t, iwg);
   if (rc != OP_OK) return rc;
   OP_AFTER_LAUNCH("conv_m16q_bf16x3", st);
   const int64_t items = (int64_t)t.total * (cop_max / 4);

@@ -147,6 +147,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
 // conv_m16w.hip: the whole-depth register-weight 7x7 kernel (OP_M16W=1 A/B aid); *taken = 0 otherwise
 int launch_conv_m16w(const SplitConvShape& s, const SplitConvGroup* g, int cop_max, hipStream_t st, int* taken);
 int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
-                    const SplitConvGroup& g1, const BigTiling& tl);
+                    const SplitConvGroup& g1, const BigTiling& tl,
+                    bool iwg);
 
 }  // namespace op

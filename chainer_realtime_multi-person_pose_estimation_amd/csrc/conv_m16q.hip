@@ -54,16 +54,24 @@ __device__ __forceinline__ void q_dma16(const void* gsrc, uint32_t lds_byte) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory");
 }
 
-template <int KS, int TR, int NTH, int PF>
-__global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
-                                                           BigTiling tl) {
+// IWG (round 6, opt-in OP_M16Q_IWG=1, measured slower at one frame): the NTH tap ranges of a chunk pair run in ONE workgroup of 4 x NTH waves (waves
+// 4r .. 4r + 3: tap range r) over the shared halo, and the ranges' accumulators are summed in LDS
+// (range 0 + range 1 + ..., exchanged through the halo's space) before the f32 partials are
+// written: the split-K index is the chunk pair alone, so the partials and the reduce launch that
+// reads them shrink NTH-fold (one frame's Mconv2-5: 8 -> 4 partials of 8.7 MB).
+template <int KS, int TR, int NTH, int PF, bool IWG = false>
+__global__ __launch_bounds__(IWG ? 256 * NTH : 256, 3) void conv_m16q_bf16x3(SplitConvShape s, SplitConvGroup g0,
+                                                                            SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS, R = KS / 2;
   constexpr int TC = 16;                 // tile columns (one 16-px block per tile row)
   constexpr int PITCH = TC + KS - 1;     // halo row pitch in 16-B slots
   constexpr int HROWS = TR + KS - 1;
   constexpr int NH = (HROWS * PITCH + 63) / 64;  // 1-KiB pieces per halo plane
   constexpr int HPLANE = NH * 1024;
-  constexpr int PIECES = 2 * NH;         // 8 planes x NH pieces over 4 waves
+  constexpr int NWV = IWG ? 4 * NTH : 4;  // waves per workgroup
+  constexpr int PIECES = 8 * NH / NWV;   // 8 planes x NH pieces over the waves
+  static_assert((8 * NH) % NWV == 0, "halo pieces split evenly over the waves");
+  static_assert(!IWG || 4 * 64 * 2 * TR * 16 <= 8 * NH * 1024, "tap-range exchange fits the halo's LDS");
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [8 planes][NH KiB]
 
   // block -> (pixel tile, weight set); weight set = (unit, split), split = (chunk pair, tap range)
@@ -72,7 +80,8 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
   const int tile = lin / nws, wsi = lin - (lin / nws) * nws;
   if (tile >= tl.per_unit) return;
   const int unit = wsi / tl.ksplit, sp = wsi - (wsi / tl.ksplit) * tl.ksplit;
-  const int cp = sp / NTH, th = sp - (sp / NTH) * NTH;
+  const int wave_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cp = IWG ? sp : sp / NTH, th = IWG ? wave_ >> 2 : sp - (sp / NTH) * NTH;
   const int grp = unit / tl.co_tiles;
   const int co0 = (unit - grp * tl.co_tiles) * 128;
   const SplitConvGroup g = grp == 0 ? g0 : g1;
@@ -88,7 +97,7 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
   const unsigned long long q_r0 = __builtin_amdgcn_s_memrealtime(), q_t0 = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = IWG ? (wave_ & 3) : wave_;  // this wave's 32-channel slice
   const int l16 = lane & 15, kg = lane >> 4;
   const int csel = kg >> 1, khalf = kg & 1;
   const int wp_in = s.w + 2 * s.pin;
@@ -117,7 +126,7 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
   // ---- B: the chunk pair's halo, (TR + 6) x (16 + 6) slots per plane, 8 planes ----
 #pragma unroll
   for (int k = 0; k < PIECES; ++k) {
-    const int j = wave + 4 * k;
+    const int j = wave_ + NWV * k;
     const int plane = j / NH, i = j - (j / NH) * NH;
     const int cj = plane >> 2, pl = plane & 3;
     const int slot = i * 64 + lane;  // slots past the window read a clamped pixel, never used
@@ -194,6 +203,33 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
   const unsigned long long q_t2 = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_sched_barrier(0);
 #endif
+  if constexpr (IWG) {
+    // the tap ranges' sums: ranges 1 .. NTH-1 hand their accumulators to range 0 through LDS (the
+    // halo's space, free once every wave is past its last tap), added in range order
+    __syncthreads();
+    float* const xch = (float*)lds;
+    for (int r = 1; r < NTH; ++r) {
+      if (th == r) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int pb = 0; pb < TR; ++pb) *(floatx4*)(xch + ((wave * 2 * TR + cb * TR + pb) * 64 + lane) * 4) = acc[cb][pb];
+      }
+      __syncthreads();
+      if (th == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int pb = 0; pb < TR; ++pb) {
+            const floatx4 o = *(const floatx4*)(xch + ((wave * 2 * TR + cb * TR + pb) * 64 + lane) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[cb][pb][e] += o[e];
+          }
+      }
+      if (r + 1 < NTH) __syncthreads();
+    }
+    if (th != 0) return;
+  }
   // ---- f32 partials of split sp: ws [split][group][pixel of the batch][wsc] ----
   const int wsc = max(g0.cop, g1.cop);
   float* const wsg = tl.ws + ((int64_t)sp * s.groups + grp) * (int64_t)tl.total * wsc;
@@ -224,14 +260,21 @@ __global__ __launch_bounds__(256, 3) void conv_m16q_bf16x3(SplitConvShape s, Spl
 }
 
 int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
-                    const SplitConvGroup& g1, const BigTiling& tl) {
+                    const SplitConvGroup& g1, const BigTiling& tl, bool iwg) {
   // OP_M16Q_LDS_KB (A/B aid): allocate at least that much LDS per workgroup (caps workgroups per CU)
   static const int lds_min = getenv("OP_M16Q_LDS_KB") ? atoi(getenv("OP_M16Q_LDS_KB")) * 1024 : 0;
   auto lds_of = [](int r) { return std::max(lds_min, 8 * (((r + 6) * 22 + 63) / 64) * 1024); };
   const dim3 grid((unsigned)(tl.per_unit * tl.units * tl.ksplit));
 #define M16Q_LAUNCH(R, T, P) \
   hipLaunchKernelGGL((conv_m16q_bf16x3<7, R, T, P>), grid, dim3(256), lds_of(R), st, s, g0, g1, tl)
-  if (tr == 4 && (pf == 2 || pf == 4) && nth >= 2 && nth <= 4) {
+  if (iwg) {  // one workgroup per chunk pair, its 2 tap ranges inside (tl.ksplit = chunk pairs)
+    if (tr == 4 && nth == 2 && pf == 2) {
+      hipLaunchKernelGGL((conv_m16q_bf16x3<7, 4, 2, 2, true>), grid, dim3(512), lds_of(4), st, s, g0, g1, tl);
+    } else {
+      set_error("conv_m16q_bf16x3 (tap ranges in one workgroup): tile rows 4, 2 tap ranges, prefetch 2 only");
+      return OP_ERR_INVALID;
+    }
+  } else if (tr == 4 && (pf == 2 || pf == 4) && nth >= 2 && nth <= 4) {
 #define M16Q_PF(P)                                  \
   if (pf == P) {                                    \
     if (nth == 2) M16Q_LAUNCH(4, 2, P);             \

@@ -323,6 +323,11 @@ struct op_ctx {
   // async frame uploads (op_upload_frames): a 2-slot device ring filled on copy_stream; the next
   // run waits for its slot's copy and moves it into d_frames on the compute stream
   hipStream_t copy_stream = nullptr;
+  // detect_precise (round 6): the small scales' forwards run on side_stream, concurrent with the large
+  // ones on the compute stream (fork / join events); while they are enqueued `stream` points at it
+  hipStream_t side_stream = nullptr;
+  hipStream_t main_stream = nullptr;  // the compute stream while `stream` is swapped to side_stream
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* d_ring[2] = {nullptr, nullptr};
   size_t ring_bytes[2] = {0, 0};
   hipEvent_t ev_up[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -440,6 +445,8 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
       // every stream that may still read the arena: the compute stream and the upload ring's copy
       // stream (which touches only d_ring, but hipFree must not race any queued work)
       OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+      if (c->main_stream) OP_HIP_CHECK(hipStreamSynchronize(c->main_stream));
+      if (c->side_stream) OP_HIP_CHECK(hipStreamSynchronize(c->side_stream));
       if (c->copy_stream) OP_HIP_CHECK(hipStreamSynchronize(c->copy_stream));
       guard_forget(c->arenas[lru].p, c->arenas[lru].bytes);
       OP_HIP_CHECK(hipFree(c->arenas[lru].p));
@@ -546,6 +553,8 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
 static int grow_buffer(op_ctx* c, void** p, size_t* cap, size_t bytes, const char* name) {
   if (bytes <= *cap) return OP_OK;
   OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->main_stream) OP_HIP_CHECK(hipStreamSynchronize(c->main_stream));
+  if (c->side_stream) OP_HIP_CHECK(hipStreamSynchronize(c->side_stream));
   if (*p) {
     guard_forget(*p, *cap + g_guard);
     OP_HIP_CHECK(hipFree(*p));
@@ -1376,6 +1385,7 @@ int op_destroy(op_ctx* c) {
   if (!c) return OP_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->side_stream) hipStreamSynchronize(c->side_stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
@@ -1418,6 +1428,13 @@ int op_destroy(op_ctx* c) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
   }
+  if (c->side_stream) {
+    (void)hipStreamSynchronize(c->side_stream);
+    splitk_ws_release(c->side_stream);
+    (void)hipStreamDestroy(c->side_stream);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (int i = 0; i < 2; ++i) {
     if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
     if (c->ev_up[i]) (void)hipEventDestroy(c->ev_up[i]);
@@ -2424,16 +2441,105 @@ __global__ __launch_bounds__(1024) void keep_plan(PostBuffers b, int first, int 
   }
 }
 
-// Keep slot fill: per frame, as keep_plan assigned it.  A frame over the batched caps keeps its
-// post-process input and batched peak counts (it is re-run alone in big mode); a frame with more
-// persons than the record holds keeps its batched result rows (they are complete: copied out as
-// they are).
+// The frame-order plan of frame i computed by its own block (keep_overflow with plan_self, packs
+// of <= kKeepSelfPlan frames): the same prefix counts as keep_plan over frames 0 .. i-1 (each block
+// reads the earlier frames' headers itself: O(n^2) reads, a few microseconds at the headline's
+// 232 frames) -- one launch fewer per pack, which the one-frame latency path pays for in full.
+constexpr int kKeepSelfPlan = 1024;
+__device__ void keep_plan_self(const PostBuffers& b, int first, int i, int max_persons, int have_src,
+                               int32_t* __restrict__ hdr, int64_t h_rows_cap, int slots) {
+  __shared__ int64_t r_rows[4];
+  __shared__ int r_res[4], r_map[4];
+  const int t = threadIdx.x;
+  auto why_of = [&](int j, int* persons) {
+    const int f = first + j;
+    const int status = b.res_hdr[4 * f];
+    *persons = b.res_hdr[4 * f + 2];
+    return status == OP_ERR_CAPACITY ? 1 : (status == OP_OK && *persons > max_persons) ? 2 : 0;
+  };
+  // rows of every earlier why-2 frame; the earlier frames needing a res / maps slot.  A why-2 frame
+  // needs a res slot iff its rows did not fit: o_j + rows_j > cap, o_j the rows of those before it
+  // (rows only grow, so once one misses, every later one misses: the count of misses is the count
+  // of why-2 frames j < i whose inclusive row sum exceeds the cap)
+  int64_t rows = 0;
+  int nres = 0, nmap = 0;
+  // pass 1: inclusive row sums need order -- each thread takes a contiguous run of earlier frames
+  const int per = (i + 255) / 256, j0 = min(i, t * per), j1 = min(i, j0 + per);
+  int64_t run = 0;
+  for (int j = j0; j < j1; ++j) {
+    int p;
+    if (why_of(j, &p) == 2) run += (int64_t)p * 55;
+  }
+  // exclusive prefix of the runs over the threads (a block scan in LDS)
+  __shared__ int64_t s_run[256];
+  s_run[t] = run;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const int64_t v = t >= d ? s_run[t - d] : 0;
+    __syncthreads();
+    s_run[t] += v;
+    __syncthreads();
+  }
+  int64_t acc = s_run[t] - run;  // rows of the why-2 frames before this thread's run
+  for (int j = j0; j < j1; ++j) {
+    int p;
+    const int w = why_of(j, &p);
+    if (w == 2) {
+      acc += (int64_t)p * 55;
+      nres += acc > h_rows_cap;
+    } else if (w == 1 && have_src) {
+      ++nmap;
+    }
+  }
+  rows = run;
+  // block sums of the run rows (total before frame i), res and map counts
+  for (int o = 32; o > 0; o >>= 1) {
+    rows += __shfl_xor(rows, o);
+    nres += __shfl_xor(nres, o);
+    nmap += __shfl_xor(nmap, o);
+  }
+  if ((t & 63) == 0) {
+    r_rows[t >> 6] = rows;
+    r_res[t >> 6] = nres;
+    r_map[t >> 6] = nmap;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int64_t o = r_rows[0] + r_rows[1] + r_rows[2] + r_rows[3];
+    const int cres = r_res[0] + r_res[1] + r_res[2] + r_res[3], cmap = r_map[0] + r_map[1] + r_map[2] + r_map[3];
+    int p;
+    const int w = why_of(i, &p);
+    const int f = first + i;
+    const int status = b.res_hdr[4 * f];
+    int off = -1;
+    if (w == 2) {
+      if (o + (int64_t)p * 55 <= h_rows_cap) off = (int)o;
+      else if (cres < slots) off = -2 - cres;
+    } else if (w == 1 && have_src) {
+      if (cmap < slots) off = cmap;
+    }
+    int32_t* h = hdr + kKeepHdr * i;
+    h[0] = status;
+    h[1] = b.res_hdr[4 * f + 1];
+    h[2] = status == OP_OK ? p : 0;
+    h[3] = w;
+    h[4] = off;
+  }
+  __syncthreads();
+}
+
+// Keep slot fill: per frame, as keep_plan (or the block itself, plan_self) assigned it.  A frame
+// over the batched caps keeps its post-process input and batched peak counts (it is re-run alone in
+// big mode); a frame with more persons than the record holds keeps its batched result rows (they
+// are complete: copied out as they are).
 __global__ __launch_bounds__(256) void keep_overflow(PostBuffers b, int first, const float* __restrict__ src,
                                                      int64_t fstride, float* __restrict__ dst, int32_t* __restrict__ cnt,
-                                                     double* __restrict__ res, const int32_t* __restrict__ hdr,
-                                                     double* __restrict__ h_rows) {
+                                                     double* __restrict__ res, int32_t* __restrict__ hdr,
+                                                     double* __restrict__ h_rows, int plan_self, int max_persons,
+                                                     int64_t h_rows_cap, int slots) {
   const int i = blockIdx.x;
   const int f = first + i;
+  if (plan_self) keep_plan_self(b, first, i, max_persons, src ? 1 : 0, hdr, h_rows_cap, slots);
   const int why = hdr[kKeepHdr * i + 3], off = hdr[kKeepHdr * i + 4];
   if (why == 2) {
     if (off == -1) return;
@@ -2542,11 +2648,15 @@ int ctx_pack_records(op_ctx* c, int first, int n, int max_persons, int64_t frame
       k.hdr_cap = hb;
     }
     RC(profiled(c, kProfOther, 0.0, 0.0, [&] {
-      hipLaunchKernelGGL(keep_plan, dim3(1), dim3(1024), 0, c->stream, c->pb, first, n, max_persons, src ? 1 : 0,
-                         k.d_hdr, k.rows_cap_now, k.slots);
-      OP_AFTER_LAUNCH("keep_plan", c->stream);
+      const char* kp_env = getenv("OP_KEEP_PLAN_KERNEL");  // test aid: 1 = the separate keep_plan launch
+      const int self = n <= kKeepSelfPlan && !(kp_env && atoi(kp_env) == 1) ? 1 : 0;
+      if (!self) {
+        hipLaunchKernelGGL(keep_plan, dim3(1), dim3(1024), 0, c->stream, c->pb, first, n, max_persons, src ? 1 : 0,
+                           k.d_hdr, k.rows_cap_now, k.slots);
+        OP_AFTER_LAUNCH("keep_plan", c->stream);
+      }
       hipLaunchKernelGGL(keep_overflow, dim3(n), dim3(256), 0, c->stream, c->pb, first, src, fstride, k.maps, k.cnt,
-                         k.res, k.d_hdr, k.d_rows_view);
+                         k.res, k.d_hdr, k.d_rows_view, self, max_persons, k.rows_cap_now, k.slots);
       OP_AFTER_LAUNCH("keep_overflow", c->stream);
       return OP_OK;
     }));
@@ -2817,7 +2927,7 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   RC(grow_buffer(c, (void**)&c->d_pmid, &c->pmid_bytes, (fused ? low_off[ns] : mid_off[ns]) * 4, "precise_mid"));
   RC(grow_buffer(c, (void**)&c->d_psum, &c->psum_bytes, (size_t)n * fplanes * 4, "precise_sum"));
   const size_t fbytes = (size_t)h * w * 3;
-  for (int k = 0; k < ns; ++k) {
+  auto run_scale = [&](int k) -> int {
     const int rw = rws[k], rh = rhs[k], pw = pws[k], ph = phs[k];
     RC(ensure_geometry(c, n, ph, pw));
     const Act& x0 = c->buf[B_X0];
@@ -2872,7 +2982,58 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
                                               pw, n, c->stream);
       }));
     }
+    return OP_OK;
+  };
+  // Round 6: the scales whose padded input is at most a quarter of the
+  // largest's (1280x720: scales 0.5 and 1.0) run on a second stream, enqueued first, so their
+  // launches -- a fraction of a round of workgroups each -- fill the rounds the large scales'
+  // launches leave partly idle.  Each scale has its own activation arena (ensure_geometry caches one
+  // per geometry, up to 6), its own region of d_pmid and, per stream, its own split-K workspace;
+  // the side stream starts after everything queued on the compute stream (the staged frames, the
+  // previous step's reads of d_pmid) and the compute stream waits for it before the scale mean.
+  // OP_PRECISE_STREAMS=1 (read per call) runs every scale on the compute stream; never under capture.
+  const char* ps_env = getenv("OP_PRECISE_STREAMS");
+  hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+  OP_HIP_CHECK(hipStreamIsCapturing(c->stream, &cap_st));
+  std::vector<int> side, mainv;
+  int64_t big = 0;
+  for (int k = 0; k < ns; ++k) big = std::max<int64_t>(big, (int64_t)phs[k] * pws[k]);
+  for (int k = 0; k < ns; ++k) {
+    const bool small = ns > 1 && 4 * (int64_t)phs[k] * pws[k] <= big;
+    (small && !(ps_env && atoi(ps_env) == 1) && cap_st == hipStreamCaptureStatusNone ? side : mainv).push_back(k);
   }
+  if (!side.empty()) {
+    if (!c->side_stream) {
+      OP_HIP_CHECK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+      OP_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    OP_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
+    OP_HIP_CHECK(hipStreamWaitEvent(c->side_stream, c->ev_fork, 0));
+    c->main_stream = c->stream;
+    c->stream = c->side_stream;
+    int rc = OP_OK;
+    for (int k : side)
+      if ((rc = run_scale(k)) != OP_OK) break;
+    c->stream = c->main_stream;
+    c->main_stream = nullptr;
+    // the join is recorded and waited for even after a failure, so no later work on the compute
+    // stream can overtake what the side stream still has queued
+    OP_HIP_CHECK(hipEventRecord(c->ev_join, c->side_stream));
+    if (rc != OP_OK) {
+      OP_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      return rc;
+    }
+    census_add(OP_CENSUS_PRECISE_SIDE);
+  }
+  for (int k : mainv) {
+    const int rc = run_scale(k);
+    if (rc != OP_OK) {
+      if (!side.empty()) OP_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      return rc;
+    }
+  }
+  if (!side.empty()) OP_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   // :462-463 / :466-467 / :469-470 every scale's crop to rh x rw and cubic to h x w, summed in scale
   // order and divided by the scale count: one pass per frame over the PAF and heat planes
   census_add(fused ? OP_CENSUS_CUBIC_FUSED : OP_CENSUS_CUBIC_TWO_PASS);

@@ -229,6 +229,40 @@ def test_c5_stream_batch_of_64_720p_frames(lib, bctx):
         assert np.array_equal(s, d["scores"]), i
 
 
+@pytest.mark.parametrize("n", [1, 16])
+def test_precise_side_stream_bit_identical(lib, monkeypatch, n):
+    """Round 6: detect_precise runs the scales whose padded input is at most a
+    quarter of the largest's (0.5 and 1.0 at 1280x720) on a second stream, concurrent with the large
+    ones; each scale has its own arena, d_pmid region and split-K workspace, so the averaged maps
+    are bit-identical to every scale on the compute stream (OP_PRECISE_STREAMS=1), in the default
+    (split-K) mode the C4 bench line runs, for the bench's 16 frames and one frame; the census
+    counts the runs that forked."""
+    from test_gpu_precise_full import _crowd_frame, _weights
+    frames = np.stack([_crowd_frame(300 + i) for i in range(n)])
+    c = lib.Context(0)
+    try:
+        c.set_weights(_weights(case_weights("posenet", 0)))
+        out = {}
+        for streams in ("1", "2", "2b"):
+            monkeypatch.setenv("OP_PRECISE_STREAMS", streams[0])
+            c.stage_frames(frames)
+            _census_npx(lib)
+            try:
+                c.run_staged_precise()
+            except IndexError:
+                pass
+            c.synchronize()
+            cen = _census_npx(lib)
+            assert cen["precise_side"] == (0 if streams == "1" else 1), (streams, cen)
+            out[streams] = c.fetch_maps(0, n)
+        monkeypatch.delenv("OP_PRECISE_STREAMS")
+        for k in ("2", "2b"):
+            for a, b in zip(out["1"], out[k]):
+                assert np.array_equal(a, b), (k, float(np.abs(a - b).max()))
+    finally:
+        c.close()
+
+
 def test_precise_staged_batch_of_16_equals_single_frames(lib):
     """The C4 line's batch (bench.py --precise: 16 frames of 1280x720, 4 scales): the per-scale
     batched forwards run NPX 8 / 10 tiles that one frame never reaches; every frame's averaged maps

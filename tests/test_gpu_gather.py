@@ -245,11 +245,15 @@ def test_keep_slots_grow_after_a_short_gather(fresh_ctx, monkeypatch):
         g.close()
 
 
-def test_keep_slot_growth_is_capped(fresh_ctx, monkeypatch):
+@pytest.mark.parametrize("plan_kernel", ["0", "1"])
+def test_keep_slot_growth_is_capped(fresh_ctx, monkeypatch, plan_kernel):
     """advisor r05: a short gather grows the next packs' keep slots, but only up to a byte ceiling
     (16 GiB of maps per gather slot; OP_KEEP_GROW_BYTES, test aid, lowers it): with a budget of 1
     byte and a 1-byte ceiling, 12 frames past max_persons get the minimum 8 slots in both gathers,
-    the same 4 frames (8-11, frame order) are reported lost both times, and the pack never fails."""
+    the same 4 frames (8-11, frame order) are reported lost both times, and the pack never fails.
+    Both frame-order planners: keep_overflow's own (packs of <= 1024 frames) and the separate
+    keep_plan launch (larger packs; OP_KEEP_PLAN_KERNEL=1 forces it)."""
+    monkeypatch.setenv("OP_KEEP_PLAN_KERNEL", plan_kernel)
     monkeypatch.setenv("OP_KEEP_ROWS_AVG", "0")
     monkeypatch.setenv("OP_KEEP_BYTES", "1")
     monkeypatch.setenv("OP_KEEP_GROW_BYTES", "1")
@@ -270,6 +274,41 @@ def test_keep_slot_growth_is_capped(fresh_ctx, monkeypatch):
             assert g.lost == 4 * (step + 1), (step, g.lost)
             assert sorted(r[0] for r in ovf if r[1] == F.STATUS_CAPACITY) == [8, 9, 10, 11], ovf
             assert F.count_persons(raw, MAXP, ovf)[1] == 4
+    finally:
+        fresh_ctx.use_staged_maps(False)
+        g.close()
+
+
+@pytest.mark.parametrize("plan_kernel", ["0", "1"])
+def test_keep_rows_then_slots_in_frame_order(fresh_ctx, monkeypatch, plan_kernel):
+    """Round 6: the frame-order plan across both keep paths.  Every frame holds
+    6 persons (> max_persons): their rows go to page-locked memory while the rows of the frames
+    before them and their own fit (OP_KEEP_ROWS_AVG=1: 55 doubles per frame of the pack, so only
+    frame 0's 330 fit), the rest to device res slots in frame order (8: a 1-byte map budget), and
+    the one frame left over -- frame 9, always -- travels as lost.  Both planners (keep_overflow's
+    own and the separate keep_plan launch) give the same split."""
+    monkeypatch.setenv("OP_KEEP_PLAN_KERNEL", plan_kernel)
+    monkeypatch.setenv("OP_KEEP_ROWS_AVG", "1")
+    monkeypatch.setenv("OP_KEEP_BYTES", "1")
+    monkeypatch.delenv("OP_KEEP_FRAMES", raising=False)
+    F = pkg_module("frames")
+    six = load_golden("six_people")
+    six_maps = np.concatenate([six["paf_low"], six["heat_low"]])
+    n = 10
+    fresh_ctx.stage_frames(np.zeros((n, 368, 368, 3), np.uint8))
+    g = F.RcclGather(fresh_ctx, F.SocketTransport(0, 1), max_persons=MAXP, timeout=60)
+    try:
+        fresh_ctx.stage_maps(np.stack([six_maps] * n))
+        fresh_ctx.use_staged_maps(True)
+        fresh_ctx.run_staged()
+        g.submit(0, n, 0, 1)
+        raw, ovf = g.wait(raw=True)
+        assert g.lost == 1, g.lost
+        assert [r[0] for r in ovf if r[1] == F.STATUS_CAPACITY] == [9], ovf
+        want = fresh_ctx.fetch_results(0, n)
+        for r in ovf:
+            if r[1] == 0:
+                assert np.array_equal(r[3], np.asarray(want[r[0]][0]).reshape(r[3].shape)), r[0]
     finally:
         fresh_ctx.use_staged_maps(False)
         g.close()

@@ -49,18 +49,26 @@ def _fixture():
     return d["x"][:1].astype(np.float32), d["paf"][0], d["heat"][0]
 
 
-@pytest.mark.parametrize("tr,nth,pf", [("4", "2", "2"), ("2", "2", "2"), ("8", "2", "2"), ("4", "3", "2"),
-                                       ("4", "4", "2"), ("4", "2", "4")])
-def test_one_frame_vs_reference_fixture(lib, qctx, monkeypatch, tr, nth, pf):
+@pytest.mark.parametrize("tr,nth,pf,iwg", [("4", "2", "2", "1"), ("4", "2", "2", "0"), ("2", "2", "2", "1"),
+                                           ("8", "2", "2", "1"), ("4", "3", "2", "1"), ("4", "4", "2", "1"),
+                                           ("4", "2", "4", "1")])
+def test_one_frame_vs_reference_fixture(lib, qctx, monkeypatch, tr, nth, pf, iwg):
+    """Every instantiation, incl. round 6's default (TR 4, 2 tap ranges in one 8-wave workgroup,
+    iwg 1) and round 5's one workgroup per (chunk pair, tap range) (iwg 0)."""
     monkeypatch.setenv("OP_M16Q_TR", tr)
     monkeypatch.setenv("OP_M16Q_NTH", nth)
     monkeypatch.setenv("OP_M16Q_PF", pf)
+    monkeypatch.setenv("OP_M16Q_IWG", iwg)
     x, want_paf, want_heat = _fixture()
     lib.conv_census(reset=True)
     paf, heat = qctx.forward(x)
     cen = lib.conv_census(reset=True)
     print("TR %s NTH %s census:" % (tr, nth), cen)
     assert cen["7x7_q"] == 25 and cen["npx"] == {}, cen  # 5 stages x Mconv1..5, all on conv_m16q
+    # the in-workgroup sum is instantiated for TR 4, 2 tap ranges, prefetch 2; with 3 or 4 tap ranges
+    # asked for, Mconv1 (6 chunk pairs: 18 / 24 splits > kMaxSplitK) falls back to 2 and takes it
+    iwg_n = 25 if (tr, nth, pf, iwg) == ("4", "2", "2", "1") else 5 if (tr, pf, iwg) == ("4", "2", "1") else 0
+    assert cen["7x7_q_iwg"] == iwg_n, cen
     e = max(_max_err(paf[0], want_paf), _max_err(heat[0], want_heat))
     print("TR %s NTH %s vs reference fixture: %.3g" % (tr, nth, e))
     assert e <= TOL, e
@@ -132,3 +140,26 @@ def test_partial_tiles_vs_oracle(lib, qctx):
     e = max(_max_err(paf, opaf), _max_err(heat, oheat))
     print("23 x 25 maps vs oracle: %.3g" % e)
     assert e <= TOL, e
+
+
+def test_in_workgroup_tap_ranges_vs_split_tap_ranges(lib, qctx, monkeypatch):
+    """Round 6: the two tap ranges of a chunk pair summed in LDS inside one workgroup (IWG, the
+    default; split K = chunk pairs) vs round 5's separate workgroups per tap range (split K = chunk
+    pairs x 2): the same products, the f32 sums re-associated, so within REL; deterministic."""
+    x, _, _ = _fixture()
+    out = {}
+    for iwg in ("1", "0", "1"):
+        monkeypatch.setenv("OP_M16Q_IWG", iwg)
+        lib.conv_census(reset=True)
+        r = qctx.forward(x)
+        cen = lib.conv_census(reset=True)
+        assert cen["7x7_q_iwg"] == (25 if iwg == "1" else 0), cen
+        if iwg in out:
+            for a, b in zip(r, out[iwg]):
+                assert np.array_equal(a, b)  # run to run: the same bits
+        out[iwg] = r
+    monkeypatch.delenv("OP_M16Q_IWG")
+    for a, b in zip(out["1"], out["0"]):
+        rel = _max_err(a, b) / max(float(np.abs(b).max()), 1e-6)
+        print("conv_m16q in-workgroup vs split tap ranges: rel %.3g" % rel)
+        assert rel <= REL, rel
