@@ -2991,7 +2991,9 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   // per geometry, up to 6), its own region of d_pmid and, per stream, its own split-K workspace;
   // the side stream starts after everything queued on the compute stream (the staged frames, the
   // previous step's reads of d_pmid) and the compute stream waits for it before the scale mean.
-  // OP_PRECISE_STREAMS=1 (read per call) runs every scale on the compute stream; never under capture.
+  // OP_PRECISE_STREAMS=1 (read per call) runs every scale on the compute stream; never under capture,
+  // nor while per-class profiling is on (op_profile: event pairs on two streams would overlap, and
+  // the per-class sums -- the 7x7 roofline's launch time -- would count the overlap twice).
   const char* ps_env = getenv("OP_PRECISE_STREAMS");
   hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
   OP_HIP_CHECK(hipStreamIsCapturing(c->stream, &cap_st));
@@ -3000,7 +3002,8 @@ static int precise_run(op_ctx* c, int n, int h, int w, int* net_w, int* net_h, b
   for (int k = 0; k < ns; ++k) big = std::max<int64_t>(big, (int64_t)phs[k] * pws[k]);
   for (int k = 0; k < ns; ++k) {
     const bool small = ns > 1 && 4 * (int64_t)phs[k] * pws[k] <= big;
-    (small && !(ps_env && atoi(ps_env) == 1) && cap_st == hipStreamCaptureStatusNone ? side : mainv).push_back(k);
+    (small && !(ps_env && atoi(ps_env) == 1) && !c->prof && cap_st == hipStreamCaptureStatusNone ? side : mainv)
+        .push_back(k);
   }
   if (!side.empty()) {
     if (!c->side_stream) {
