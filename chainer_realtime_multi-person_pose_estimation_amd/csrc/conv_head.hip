@@ -16,6 +16,7 @@
 // them), issued a K step (GEMM2) or a chunk (GEMM1) ahead.  Mconv6+7 (one chunk): the intermediate
 // overwrites the input tile, 33 KiB LDS, 4 workgroups per CU; conv5_4+5 (4 chunks): 67.5 KiB, 2.
 #include "common.hpp"
+#include "conv_big.hpp"
 
 namespace op {
 
@@ -48,7 +49,15 @@ __device__ __forceinline__ floatx4 mfma3(const bf16x8h& ah, const bf16x8h& al, c
 // TPW (round 4, opt-in OP_HEAD_TPW, measured slower): 64-px tiles per workgroup, one after the other.  Mconv6 + Mconv7 (ONE) has a
 // single 128-channel chunk, so a wave's GEMM1 weight fragments (64 KiB per workgroup, re-read from
 // L2 by every workgroup: ~1 GB per 232-frame launch) are loaded once for TPW tiles.
-template <int NB2, bool ONE, int PXB = 1, int TPW = 1>
+// PL (round 6): channel-group-planar X / T tiles, [8-ch group][hi, lo][px][16 B].
+// A ds_read_b128 lane group (above) then reads 16 consecutive pixels' 16-B pieces of planes that
+// start a multiple of 256 B apart: 64 distinct banks, no swizzle; the T write pairs rows with
+// v_permlane16_swap (split_pair_swap) into one 16-B store per lane, 8 consecutive pixels per
+// ds_write_b128 cycle.  X's lo planes hold pixel px at slot px ^ 4 (a lane group's read stays a
+// permutation of 16 slots), so the copy of a [pixel][channels] input can give 8 consecutive lanes
+// the hi and lo pieces of 4 pixels (64-B runs of each pixel per 16 lanes) and still write 8 slots.
+// (Round 6: 8 pixels x 16-B pieces per 16 lanes made conv5_4+5's copy 14 % slower.)
+template <int NB2, bool ONE, int PXB = 1, int TPW = 1, int PL = 0>
 #ifndef HEAD_TPW_OCC
 #define HEAD_TPW_OCC 3  // workgroups per CU the TPW > 1 forms are built for (a1 stays live across tiles)
 #endif
@@ -66,6 +75,7 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
   const int total = s.n * hw;
   constexpr int xpitch = CI * 4 + 16;  // +16 B: consecutive pixels start 4 banks apart
   constexpr int tpitch = 128 * 4 + 16;
+  constexpr int plane = kPx * 16;  // PL: bytes of one (group, hi | lo) plane
   char* const X = lds;
   char* const T = ONE ? lds : lds + kPx * xpitch;  // ONE (co1 = 128): T overwrites X after GEMM1
   const int lane = threadIdx.x & 63;
@@ -105,14 +115,24 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
     constexpr int pieces = CI / 4;
     const int64_t pcs = split_piece_stride(s.in_planar, hp_in, wp_in), pxs = split_pixel_stride(s.in_planar, s.cs_in);
     for (int i = threadIdx.x; i < kPx * pieces; i += 256) {
-      const int px = s.in_planar ? i % kPx : i / pieces;
-      const int pc = s.in_planar ? i / kPx : i - px * pieces;
+      int px, pc;
+      if ((PL & 1) && !s.in_planar) {  // lanes (hi | lo piece, 4 pixels, 8 piece pairs): 64-B runs read
+        const int lo = i & 63, hi = i >> 6;
+        px = ((lo >> 1) & 3) + 4 * (hi % (kPx / 4));
+        pc = (lo & 1) + 2 * (lo >> 3) + 16 * (hi / (kPx / 4));
+      } else {
+        px = s.in_planar ? i % kPx : i / pieces;
+        pc = s.in_planar ? i / kPx : i - px * pieces;
+      }
       const int P = min(P0 + px, total - 1);
       const int f = P / hw, pp = P - f * hw;
       const int y = pp / s.w, x = pp - y * s.w;
       const char* src = (const char*)g.in + (int64_t)f * hp_in * wp_in * s.cs_in * 4 +
                         ((int64_t)(y + s.pin) * wp_in + x + s.pin) * pxs + pc * pcs;
-      *(uint4*)(X + px * xpitch + (((pc >> 1) ^ head_swz(px)) * 32 + (pc & 1) * 16)) = *(const uint4*)src;
+      if constexpr ((PL & 1) != 0)
+        *(uint4*)(X + pc * plane + (px ^ (pc & 1) * 4) * 16) = *(const uint4*)src;
+      else
+        *(uint4*)(X + px * xpitch + (((pc >> 1) ^ head_swz(px)) * 32 + (pc & 1) * 16)) = *(const uint4*)src;
     }
   }
   __syncthreads();
@@ -134,9 +154,10 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int pb = 0; pb < 4 * PXB; ++pb) {
-        const char* xb = X + (pb * 16 + l16) * xpitch + ((4 * k + kg) ^ head_swz(l16)) * 32;
+        const char* xb = (PL & 1) ? X + (4 * k + kg) * 2 * plane + (pb * 16 + l16) * 16
+                            : X + (pb * 16 + l16) * xpitch + ((4 * k + kg) ^ head_swz(l16)) * 32;
         const bf16x8h bh = *(const bf16x8h*)xb;
-        const bf16x8h bl = *(const bf16x8h*)(xb + 16);
+        const bf16x8h bl = *(const bf16x8h*)((PL & 1) ? xb + plane + ((l16 ^ 4) - l16) * 16 : xb + 16);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) acc1[cb][pb] = mfma3(a1[k][cb][0], a1[k][cb][1], bh, bl, acc1[cb][pb]);
       }
@@ -161,6 +182,13 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
       const floatx4 bv = *(const floatx4*)(g.b1 + chunk + cl);
 #pragma unroll
       for (int pb = 0; pb < 4 * PXB; ++pb) {
+        if constexpr ((PL & 2) != 0) {
+          floatx4 v;
+          uint32_t own[4], w[4];
+          split_pair_swap(acc1[cb][pb], bv, 1, v, own, w);
+          *(uint4*)(T + ((cl >> 3) * 2 + (kg & 1)) * plane + (pb * 16 + l16) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+          continue;
+        }
         u16x4h vh, vl;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -189,9 +217,10 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
       if (k + 1 < 4) load_a2(k + 1);
 #pragma unroll
       for (int q = 0; q < PXB; ++q) {
-        const char* tb = T + ((wave + 4 * q) * 16 + l16) * tpitch + ((4 * k + kg) ^ head_swz(l16)) * 32;
+        const char* tb = (PL & 2) ? T + (4 * k + kg) * 2 * plane + ((wave + 4 * q) * 16 + l16) * 16
+                            : T + ((wave + 4 * q) * 16 + l16) * tpitch + ((4 * k + kg) ^ head_swz(l16)) * 32;
         const bf16x8h bh = *(const bf16x8h*)tb;
-        const bf16x8h bl = *(const bf16x8h*)(tb + 16);
+        const bf16x8h bl = *(const bf16x8h*)(tb + ((PL & 2) ? plane : 16));
 #pragma unroll
         for (int j = 0; j < NB2; ++j) acc2[q][j] = mfma3(cur[j][0], cur[j][1], bh, bl, acc2[q][j]);
       }
@@ -238,6 +267,28 @@ __global__ __launch_bounds__(256, ONE ? (TPW > 1 ? HEAD_TPW_OCC : 4 / PXB) : 2 /
   }
 }
 
+template <int NB2, bool ONE, int PXB, int PL>
+static int launch_head_pl1(dim3 grid, int lds, hipStream_t st, const HeadShape& s, const HeadGroup& a,
+                            const HeadGroup& b, int per) {
+  static bool attr = false;
+  if (!attr) {
+    OP_HIP_CHECK(hipFuncSetAttribute((const void*)conv_head_bf16x3<NB2, ONE, PXB, 1, PL>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_head_bf16x3<NB2, ONE, PXB, 1, PL>), grid, dim3(256), lds, st, s, a, b, per);
+  return OP_OK;
+}
+
+template <int NB2, bool ONE, int PXB>
+static int launch_head_pl(int pl, dim3 grid, int lds, hipStream_t st, const HeadShape& s, const HeadGroup& a,
+                           const HeadGroup& b, int per) {
+  static_assert(PXB == 1, "planar tiles: 64-px workgroups");
+  if (pl == 1) return launch_head_pl1<NB2, ONE, PXB, 1>(grid, lds, st, s, a, b, per);
+  if (pl == 2) return launch_head_pl1<NB2, ONE, PXB, 2>(grid, lds, st, s, a, b, per);
+  return launch_head_pl1<NB2, ONE, PXB, 3>(grid, lds, st, s, a, b, per);
+}
+
 template <int NB2, int PXB>
 static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st) {
   constexpr int kPx = kHeadPx * PXB;
@@ -251,6 +302,14 @@ static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st
   int tpw = 1;
   if (one && PXB == 1 && (tpw_env == 2 || tpw_env == 4)) tpw = tpw_env;
   const int per = (tiles + tpw - 1) / tpw;
+  // channel-group-planar LDS tiles (PL, round 6): bit 0 X, bit 1 T.  OP_HEAD_PLANAR (Mconv6+7) and
+  // OP_HEAD_PLANAR1 (conv5_4+5) = 0..3, read per launch (the bit-identity test flips them in one
+  // process).  Defaults: Mconv6+7 3 (LDS bank conflicts 4.00 -> 0.00 per LDS instruction at equal
+  // time, 259-260 us per 232-frame launch either way); conv5_4+5 0, its four-chunk loop ran 10-12 %
+  // slower with ANY planar bit (850-878 vs 778 us; the compiler reorders the whole loop, and
+  // sched_barriers between the phases gave 823-833 us) -- profiles/r06/ab_r06j_head_planar.log.
+  const char* pl_env = getenv(one ? "OP_HEAD_PLANAR" : "OP_HEAD_PLANAR1");
+  const int pl = (PXB == 1 && tpw == 1) ? (pl_env ? (atoi(pl_env) & 3) : (one ? 3 : 0)) : 0;
   const int lds = kPx * (128 * 4 + 16) * (one ? 1 : 2);
   static bool attr = false;
   if (!attr) {
@@ -264,7 +323,15 @@ static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  if (one && tpw == 4)
+  const dim3 grid((unsigned)(per * s.groups));
+  int rc = OP_OK;
+  if constexpr (PXB == 1) {
+    if (pl && one) rc = launch_head_pl<NB2, true, PXB>(pl, grid, lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], per);
+    else if (pl) rc = launch_head_pl<NB2, false, PXB>(pl, grid, lds, st, s, g[0], s.groups > 1 ? g[1] : g[0], per);
+  }
+  if (rc) return rc;
+  if (pl) {
+  } else if (one && tpw == 4)
     hipLaunchKernelGGL((conv_head_bf16x3<NB2, true, PXB, 4>), dim3((unsigned)(per * s.groups)), dim3(256), lds, st, s,
                        g[0], s.groups > 1 ? g[1] : g[0], per);
   else if (one && tpw == 2)

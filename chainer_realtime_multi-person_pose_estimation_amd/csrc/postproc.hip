@@ -820,6 +820,17 @@ __device__ __forceinline__ int reflect_near(int i, int L) {
   return i < 0 ? 0 : (i >= L ? L - 1 : i);  // L > radius: one reflection suffices
 }
 
+// Smallest (hi = false) or largest (hi = true) of reflect_near(a, L) over a .. a + n - 1: the
+// identity on 0 .. L-1, a decreasing piece below 0 (values 0 .. -a-1) and above L - 1 (2L-1-e .. L-1).
+__device__ __forceinline__ int reflect_span(int a, int n, int L, bool hi) {
+  const int e = a + n - 1;
+  int lo = a < 0 ? 0 : a, up = e > L - 1 ? L - 1 : e;
+  if (e > L - 1) lo = min(lo, 2 * L - 1 - e);
+  if (a < 0) up = max(up, -a - 1);
+  const int v = hi ? up : lo;
+  return v < 0 ? 0 : (v > L - 1 ? L - 1 : v);
+}
+
 struct HeatLow {  // heat channels of the low-res stage output, upsampled on the fly
   static constexpr bool kLow = true;
   MapSource src;
@@ -852,18 +863,35 @@ __device__ __forceinline__ bool may_reach(float v, float thresh) {
 // tiles per plane.  Only for launches of >= 8 frames (xcd_major): with fewer, every tile of a frame
 // would run on one XCD (one frame: 32 of 256 CUs, 7/8 of the grid exiting at once), so small
 // launches take the plain order, which spreads a frame's tiles over the whole chip (advisor r04).
+// true when NO thread of the block has `live` (a barrier for every thread): a ballot per wave and one
+// store per wave with a live lane -- __syncthreads_or had every lane OR into one LDS word, 64 lanes
+// of an instruction on one bank (round 6).  *flag: zeroed before a barrier that precedes this call.
+__device__ __forceinline__ bool block_none(bool live, int* flag) {
+  if (__ballot(live) && (threadIdx.x & 63) == 0) *flag = 1;
+  __syncthreads();
+  return *flag == 0;
+}
+
 template <class Src, int R>
 __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const double* __restrict__ w, int rr,
                                                   float thresh, int cap, int32_t* __restrict__ stage_key,
                                                   float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt,
                                                   int n_frames, int tx, int ty, int xcd_major) {
-  constexpr int kTP = kFU + 2;  // vertical-pass output pitch (16-byte aligned rows)
+  // vertical-pass output pitch: 33 16-B slots (round 6; was kFU + 2 = 100 floats).  The horizontal
+  // pass gives lane i the slot (i / 17) * pitch + i % 17 = i + 16 * (i / 17) (17 four-column groups
+  // per row), so with a pitch of 1 (mod 16) slots every ds_read_b128 lane group reads 16 distinct
+  // slots mod 16: conflict-free (at 25 slots the rows a group spans collided 2-way)
+  constexpr int kTP = 4 * 33;
+  static_assert(kTP >= kFU + 2 && (kTP / 4) % 16 == 1, "horizontal-pass pitch");
   constexpr int kHP = kFT + 4;  // filtered-map pitch
   constexpr int NB = 4;         // outputs per thread in the register-blocked passes
   __shared__ float up[(kFU + NB) * kFU];         // upsampled region; reused for the filtered map
   __shared__ float tmp[(kFT + 2 + 1) * kTP];     // vertical-pass output; low-res window before that
-  __shared__ AxisTap rt[kFU], ct[kFU];
-  __shared__ int wlo[2], whi[2];
+  // the region's row / column taps: weights (16 B, read by ds_read_b128) apart from the indices
+  // (4 B) -- a 24-B AxisTap array put lanes 16 apart on one bank for the i0 reads (round 6)
+  __shared__ double2 rtw[kFU], ctw[kFU];
+  __shared__ int rti[kFU], cti[kFU];
+  __shared__ int any_live;
   const int r = R > 0 ? R : rr;
   const int per_frame = tx * ty * OP_N_JOINTS;
   const int lin = blockIdx.x;
@@ -885,23 +913,26 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
   const int ur = hr + 2 * r, uc = hc + 2 * r;
   const int uy0 = y0 - 1 - r, ux0 = x0 - 1 - r;
   if constexpr (Src::kLow) {
-    if (threadIdx.x < 2) {
-      wlo[threadIdx.x] = 0x7fffffff;
-      whi[threadIdx.x] = -1;
-    }
-    __syncthreads();
     for (int i = threadIdx.x; i < ur + uc; i += kFN) {
       const bool row = i < ur;
       const int k = row ? i : i - ur;
       const AxisTap t = row ? axis_tap(reflect_near(uy0 + k, mh), src.lh, mh)
                             : axis_tap(reflect_near(ux0 + k, mw), src.lw, mw);
-      (row ? rt : ct)[k] = t;
-      atomicMin(&wlo[row ? 0 : 1], t.i0);
-      atomicMax(&whi[row ? 0 : 1], t.i0 + 1);
+      (row ? rtw : ctw)[k] = make_double2(t.d1, t.d0);
+      (row ? rti : cti)[k] = t.i0;
     }
+    if (threadIdx.x == 0) any_live = 0;  // ordered before the flag stores by the barrier below
     __syncthreads();
-    const int wy = wlo[0], wx = wlo[1];
-    const int nwy = whi[0] - wy + 1, nwx = whi[1] - wx + 1;
+    // low-res window rows wy .. wy + nwy - 1 (columns likewise): the taps' i0 .. i0 + 1 over the
+    // region.  i0 is non-decreasing in the image row, so its extremes come from the extreme rows
+    // the reflected region reaches -- computed by every thread (round 6: the bounds were reduced
+    // with LDS atomics by every tap, 64 lanes on one word, the bulk of this kernel's bank-conflict
+    // cycles)
+    const int wy = axis_tap(reflect_span(uy0, ur, mh, false), src.lh, mh).i0;
+    const int wx = axis_tap(reflect_span(ux0, uc, mw, false), src.lw, mw).i0;
+    const int nwy = axis_tap(reflect_span(uy0, ur, mh, true), src.lh, mh).i0 + 2 - wy;
+    const int nwx = axis_tap(reflect_span(ux0, uc, mw, true), src.lw, mw).i0 + 2 - wx;
+
     const bool staged = nwy <= kFW && nwx <= kFW;  // block-uniform
     const LowMap m = low_map(src.src, src.lw, f);
     const int c = src.src.heat_off + j;
@@ -916,10 +947,18 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
       }
     // No low-res value of the window can lift the upsampled + smoothed tile above the peak
     // threshold: the tile has no peak, skip the passes (result identical, see may_reach).
-    if (!__syncthreads_or(live)) return;
+    if (block_none(live, &any_live)) return;
     for (int i = threadIdx.x; i < ur * uc; i += kFN) {
       const int ly = i / uc, lx = i - ly * uc;
-      const UpTap t = up_tap2(rt[ly], ct[lx]);
+      AxisTap ty, tx;
+      const double2 wy2 = rtw[ly], wx2 = ctw[lx];
+      ty.d1 = wy2.x;
+      ty.d0 = wy2.y;
+      ty.i0 = rti[ly];
+      tx.d1 = wx2.x;
+      tx.d0 = wx2.y;
+      tx.i0 = cti[lx];
+      const UpTap t = up_tap2(ty, tx);
       float v;
       if (staged) {
         const float* q = win + (t.v0 - wy) * nwx + (t.u0 - wx);
@@ -937,7 +976,7 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
       up[ly * kFU + lx] = v;
       live |= may_reach(v, thresh);
     }
-    if (!__syncthreads_or(live)) return;
+    if (!__syncthreads_or(live)) return;  // (HeatFull: the precise path's full-resolution planes)
   }
   __syncthreads();
   if constexpr (R > 0) {

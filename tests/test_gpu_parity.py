@@ -216,6 +216,25 @@ def test_fused_heads_equal_two_launches(ctx, prec, monkeypatch):
             assert float(np.abs(a - b).max()) <= 1e-4 * max(1.0, float(np.abs(b).max()))
 
 
+@pytest.mark.parametrize("n,pl", [(1, 3), (3, 1), (3, 2), (3, 3)])
+def test_head_lds_layouts_bit_identical(ctx, n, pl, monkeypatch):
+    """conv_head.hip keeps its input (X) and intermediate (T) tiles in LDS either as pixel rows
+    (round 5) or as channel-group planes (round 6: no bank conflicts); OP_HEAD_PLANAR (Mconv6+7) /
+    OP_HEAD_PLANAR1 (conv5_4+5) = bit 0 X planar, bit 1 T planar.  Only the LDS addresses differ, so
+    every stage's maps are BIT-IDENTICAL; 46 x 62 maps leave a partial last 64-pixel tile, and both
+    the chunk-planar (stages 2-6) and [pixel][channels] (stage 1) head inputs are read."""
+    rng = np.random.default_rng(22)
+    x = rng.uniform(-0.5, 0.5, (n, 3, 184, 248)).astype(np.float32)
+    ctx.set_precision("bf16x3")
+    outs = []
+    for v in (pl, 0):
+        monkeypatch.setenv("OP_HEAD_PLANAR", str(v))
+        monkeypatch.setenv("OP_HEAD_PLANAR1", str(v))
+        outs.append(ctx.forward(x))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
 def test_detect_equals_stagewise_oracle_composition(pkg, rand_weights):
     """PoseDetector(img) == oracle post-process of the GPU forward of the GPU-preprocessed image."""
     det = pkg.PoseDetector("posenet", model=rand_weights, device=0)
