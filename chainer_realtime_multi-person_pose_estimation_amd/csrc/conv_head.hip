@@ -304,12 +304,12 @@ static int launch_head_px(const HeadShape& s, const HeadGroup* g, hipStream_t st
   const int per = (tiles + tpw - 1) / tpw;
   // channel-group-planar LDS tiles (PL, round 6): bit 0 X, bit 1 T.  OP_HEAD_PLANAR (Mconv6+7) and
   // OP_HEAD_PLANAR1 (conv5_4+5) = 0..3, read per launch (the bit-identity test flips them in one
-  // process).  Defaults: Mconv6+7 3 (LDS bank conflicts 4.00 -> 0.00 per LDS instruction at equal
-  // time, 259-260 us per 232-frame launch either way); conv5_4+5 0, its four-chunk loop ran 10-12 %
-  // slower with ANY planar bit (850-878 vs 778 us; the compiler reorders the whole loop, and
-  // sched_barriers between the phases gave 823-833 us) -- profiles/r06/ab_r06j_head_planar.log.
+  // process).  Default 3 for both: LDS bank conflicts 4.00 / 4.48 -> 0.00 per LDS instruction.  At
+  // equal time only with conv_head.o built under max-ilp (Makefile): under the default scheduler
+  // conv5_4+5's four-chunk loop ran 10-12 % slower with ANY planar bit (the compiler reordered the
+  // whole loop), profiles/r06/ab_r06j_head_planar.log.
   const char* pl_env = getenv(one ? "OP_HEAD_PLANAR" : "OP_HEAD_PLANAR1");
-  const int pl = (PXB == 1 && tpw == 1) ? (pl_env ? (atoi(pl_env) & 3) : (one ? 3 : 0)) : 0;
+  const int pl = (PXB == 1 && tpw == 1) ? (pl_env ? (atoi(pl_env) & 3) : 3) : 0;
   const int lds = kPx * (128 * 4 + 16) * (one ? 1 : 2);
   static bool attr = false;
   if (!attr) {
