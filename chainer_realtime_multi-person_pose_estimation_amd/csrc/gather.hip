@@ -229,7 +229,12 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
   RC(ctx_pack_records(ctx, first, n, max_persons, frame_base, frame_stride, g->d_rec[k], &cst, k));
   OP_HIP_CHECK(hipEventRecord(g->ev_packed[k], cst));
   OP_HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_packed[k], 0));
-  ncclResult_t r = ncclGather(g->d_rec[k], g->rank == 0 ? g->d_all[k] : nullptr, mine, ncclUint8, 0, g->comm, g->stream);
+  // one rank: the gather is the identity, so the root's D2H copy reads the packed records directly
+  // (round 6: the one-rank ncclGather ran as an 11-us copy kernel per step)
+  const bool alone = g->world == 1;
+  ncclResult_t r = alone ? ncclSuccess
+                         : ncclGather(g->d_rec[k], g->rank == 0 ? g->d_all[k] : nullptr, mine, ncclUint8, 0, g->comm,
+                                      g->stream);
   if (r != ncclSuccess && r != ncclInProgress) return nccl_fail("ncclGather", r);
   if (r == ncclInProgress) {
     // non-blocking communicator: the gather may still be on its way into g->stream; the root's D2H
@@ -240,7 +245,8 @@ int op_comm_gather_results(op_comm* g, op_ctx* ctx, int32_t first, int32_t n, in
       return ae == ncclSuccess ? 1 : 0;  // an error state is reported (and aborted) by wait_for
     }));
   }
-  if (g->rank == 0) OP_HIP_CHECK(hipMemcpyAsync(g->h_all[k], g->d_all[k], all, hipMemcpyDeviceToHost, g->stream));
+  if (g->rank == 0)
+    OP_HIP_CHECK(hipMemcpyAsync(g->h_all[k], alone ? g->d_rec[k] : g->d_all[k], all, hipMemcpyDeviceToHost, g->stream));
   OP_HIP_CHECK(hipEventRecord(g->ev_done[k], g->stream));
   g->queued[k] = n * g->world;
   g->rbytes[k] = rb;
