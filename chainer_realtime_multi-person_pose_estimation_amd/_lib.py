@@ -28,7 +28,7 @@ EXPORTED = (
     "op_set_precision", "op_get_precision", "op_fetch_results", "op_fetch_maps", "op_upload_frames", "op_upload_wait", "op_conv_census", "op_host_alloc", "op_host_free",
     "op_pack_results", "op_comm_unique_id", "op_comm_create", "op_comm_destroy", "op_comm_gather_results",
     "op_comm_wait", "op_comm_overflow", "op_comm_overflow_result", "op_detect_precise", "op_resize_cubic",
-    "op_set_conv_algo", "op_set_stage_layout", "op_set_batch_invariant", "op_profile_classes", "op_run_staged_precise",
+    "op_set_conv_algo", "op_set_stage_layout", "op_set_batch_invariant", "op_set_peak_mode", "op_profile_classes", "op_run_staged_precise",
     "op_cpm_layer_count", "op_cpm_layer_info", "op_cpm_create", "op_cpm_destroy", "op_cpm_set_weights",
     "op_cpm_forward", "op_cpm_peaks", "op_cpm_detect", "op_cpm_detect_batch", "op_cpm_set_batch_invariant",
     "op_train_create", "op_train_destroy", "op_train_set_weights", "op_train_get_weights", "op_train_set_hyper",
@@ -37,6 +37,7 @@ EXPORTED = (
 ARCH = {"facenet": 1, "handnet": 2}
 MAX_SCALES = 8
 PRECISION = {"fp32": 0, "bf16x3": 1}
+PEAK_BRANCH = {"cpu": 0, "gpu": 1}  # OP_PEAKS_CPU_BRANCH / OP_PEAKS_GPU_BRANCH
 
 
 class OpParams(ctypes.Structure):
@@ -90,6 +91,7 @@ def lib():
         "op_set_conv_algo": ([P, I32], ctypes.c_int),
         "op_set_stage_layout": ([P, I32], ctypes.c_int),
         "op_set_batch_invariant": ([P, I32], ctypes.c_int),
+        "op_set_peak_mode": ([P, I32, I32], ctypes.c_int),
         "op_profile_classes": ([P, I32], ctypes.c_int),
         "op_resize_cubic": ([P, P, I32, I32, I32, I32, P, I32, I32], ctypes.c_int),
         "op_preprocess": ([P, P, I32, I32, I64, I32, I32, P], ctypes.c_int),
@@ -372,6 +374,16 @@ class Context(object):
         """Chunk-planar (1, default) or [row][col][channels] (0) 7x7 stage tensors
         (include/openpose_hip.h: op_set_stage_layout); the maps are bit-identical either way."""
         check(lib().op_set_stage_layout(self.h, 1 if planar else 0), "op_set_stage_layout")
+
+    def set_peak_mode(self, branch="cpu", ksize=None):
+        """Peak semantics of the single-scale post-process (include/openpose_hip.h: op_set_peak_mode):
+        'cpu' (default; pose_detector.py:82-110) or 'gpu', the reference's GPU branch
+        (pose_detector.py:111-132: ksize x ksize unnormalised Gaussian with zero padding, >= NMS;
+        ksize defaults to params['ksize'] = 17)."""
+        if branch not in PEAK_BRANCH:
+            raise ValueError("peak branch %r: 'cpu' or 'gpu'" % (branch,))
+        k = int(ksize if ksize is not None else 17)
+        check(lib().op_set_peak_mode(self.h, PEAK_BRANCH[branch], k), "op_set_peak_mode")
 
     def set_batch_invariant(self, enable=True):
         """One accumulation order for every batch size (include/openpose_hip.h: op_set_batch_invariant);

@@ -293,15 +293,21 @@ struct PostBuffers {
   double* res_scores;  // [B][maxs]
   double* res_subsets; // [B][maxs][20] kept subset rows (grouping_key_points output)
   int32_t* res_hdr;    // [B][4]: status, n_peaks, n_persons, reserved
-  double* gauss_w;     // [21] device copy of the Gaussian taps
+  double* gauss_w;     // [kGaussTable] device Gaussian taps: the CPU branch's 2r+1 at 0, the GPU branch's at kGaussGpuOff
   unsigned* used;      // big mode only (else null): [B][19][2][ceil(maxp/32)] greedy used-peak bitsets
 };
+
+constexpr int kGaussTable = 128;  // doubles in PostBuffers::gauss_w
+constexpr int kGaussGpuOff = 64;  // the GPU-branch taps' offset in it
+constexpr int kMaxGaussR = 16;    // largest radius of the tiled peak kernel (postproc.hip kMaxR)
 
 struct PostShape {
   int32_t n;             // frames
   int32_t lh, lw;        // network map size (low res)
   int32_t mh, mw;        // post-process map size
   int32_t radius;        // Gaussian radius (10)
+  int32_t peak_mode;     // op_set_peak_mode: 1 = GPU-branch peaks in the single-scale (HeatLow) path
+  int32_t gpu_radius;    // its Gaussian radius (ksize / 2 = 8)
   double img_len;        // distance-prior length (map_w, pose_detector.py:511)
   double sx, sy;         // output rescale (orig_w / map_w, orig_h / map_h; 1 in precise mode)
   float peak_thresh;

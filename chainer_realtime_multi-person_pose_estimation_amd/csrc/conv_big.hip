@@ -755,13 +755,15 @@ static int launch_m16k(const SplitConvShape& s, const SplitConvGroup* g, const B
   t.ksplit = 1;
   t.ws = nullptr;
   static const int ks_force = getenv("OP_M16_KSPLIT") ? atoi(getenv("OP_M16_KSPLIT")) : 0;  // A/B aid: 1 = off
+  // A/B aid: the split launch's workgroup cap (default 512 = two per CU)
+  static const int split_wg = getenv("OP_M16K_SPLIT_WG") ? atoi(getenv("OP_M16K_SPLIT_WG")) : 512;
   if (s.splitk && (!pool || s.groups == 1)) {
     const int pairs = s.c16 / 2;
     int S = 1;
     if (ks_force > 0) S = pairs % ks_force == 0 ? ks_force : 1;
     else
       for (int cand : {8, 4, 2})
-        if (pairs % cand == 0 && (int)blocks * cand <= 512) {
+        if (pairs % cand == 0 && (int)blocks * cand <= split_wg) {
           S = cand;
           break;
         }

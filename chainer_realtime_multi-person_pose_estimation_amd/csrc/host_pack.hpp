@@ -74,4 +74,18 @@ inline int gaussian_taps(double sigma, std::vector<double>& w) {
   return r;
 }
 
+// The GPU branch's kernel (pose_detector.py:38-44, built at :34 with params 'gaussian_sigma' /
+// 'ksize'): K[dy][dx] = exp(-0.5 (dx^2 + dy^2) / sigma^2) / (2 pi sigma^2) over ksize x ksize, NOT
+// normalised, is the outer product g g^T of g(d) = exp(-0.5 d^2 / sigma^2) / sqrt(2 pi sigma^2),
+// d = -r .. r, r = ksize / 2: w = g (2r + 1 doubles), returns r.  The device filter runs the two
+// 1-D passes (f64, f32 between them) instead of the reference's 2-D f32 convolution: the same
+// products up to rounding (~1e-7 relative, tests/test_gpu_peak_mode.py).
+inline int gpu_branch_taps(double sigma, int ksize, std::vector<double>& w) {
+  const int r = ksize / 2;
+  w.assign(2 * r + 1, 0.0);
+  const double norm = std::sqrt(2.0 * 3.14159265358979323846 * sigma * sigma);
+  for (int i = 0; i <= 2 * r; ++i) w[i] = std::exp(-0.5 * (double)((i - r) * (i - r)) / (sigma * sigma)) / norm;
+  return r;
+}
+
 }  // namespace op

@@ -810,6 +810,7 @@ __global__ __launch_bounds__(64) void grouping(PostShape s, PostBuffers b) {
 // reference's correlate1d reads for the tap (pose_detector.py:84, scipy mode='reflect').
 constexpr int kFT = 64;                    // output tile edge
 constexpr int kMaxR = 16;                  // max Gaussian radius of the tiled kernel
+static_assert(kMaxR == kMaxGaussR, "op_set_peak_mode checks ksize against kMaxGaussR");
 constexpr int kFU = kFT + 2 + 2 * kMaxR;   // LDS region edge (upsampled map)
 constexpr int kFW = 48;                    // low-res window edge staged in LDS
 constexpr int kFN = 512;                   // threads per block (2 blocks / CU by LDS)
@@ -872,7 +873,12 @@ __device__ __forceinline__ bool block_none(bool live, int* flag) {
   return *flag == 0;
 }
 
-template <class Src, int R>
+// G (round 6, op_set_peak_mode): the reference's GPU branch (pose_detector.py:111-132) -- the map
+// zero-padded instead of reflected (F.convolution_2d pad = ksize / 2, :112-113), w = the 1-D factor
+// of its unnormalised ksize x ksize kernel (host_pack.hpp gpu_branch_taps), and >= instead of > in
+// the 4-neighbour test (:123-126); the threshold stays strict (:123).  Only HeatLow (the single-scale
+// path): the reference's precise path and standalone calls hand it NumPy arrays (CPU branch).
+template <class Src, int R, bool G = false>
 __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const double* __restrict__ w, int rr,
                                                   float thresh, int cap, int32_t* __restrict__ stage_key,
                                                   float* __restrict__ stage_score, int32_t* __restrict__ peak_cnt,
@@ -892,6 +898,7 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
   __shared__ double2 rtw[kFU], ctw[kFU];
   __shared__ int rti[kFU], cti[kFU];
   __shared__ int any_live;
+  static_assert(!G || Src::kLow, "GPU-branch peaks: single-scale maps only");
   const int r = R > 0 ? R : rr;
   const int per_frame = tx * ty * OP_N_JOINTS;
   const int lin = blockIdx.x;
@@ -965,6 +972,10 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
         v = up_combine(t, q[0], q[1], q[nwx], q[nwx + 1]);
       } else {
         v = up_sample(m, c, t);
+      }
+      if constexpr (G) {  // zero padding: region rows / columns outside the map hold 0
+        const int yy = uy0 + ly, xx = ux0 + lx;
+        if (yy < 0 || yy >= mh || xx < 0 || xx >= mw) v = 0.0f;
       }
       up[ly * kFU + lx] = v;
     }
@@ -1064,8 +1075,11 @@ __global__ __launch_bounds__(kFN) void heat_fused(Src src, int mh, int mw, const
     const int y = y0 + ly - 1, x = x0 + lx - 1;
     if (y >= mh || x >= mw) continue;
     const float v = hm[ly * P + lx];
-    if (v > thresh && v > hm[(ly - 1) * P + lx] && v > hm[(ly + 1) * P + lx] && v > hm[ly * P + lx - 1] &&
-        v > hm[ly * P + lx + 1]) {
+    const bool peak = G ? (v > thresh && v >= hm[(ly - 1) * P + lx] && v >= hm[(ly + 1) * P + lx] &&
+                           v >= hm[ly * P + lx - 1] && v >= hm[ly * P + lx + 1])
+                        : (v > thresh && v > hm[(ly - 1) * P + lx] && v > hm[(ly + 1) * P + lx] &&
+                           v > hm[ly * P + lx - 1] && v > hm[ly * P + lx + 1]);
+    if (peak) {
       const int slot = atomicAdd(peak_cnt + fj, 1);
       if (slot < cap) {
         stage_key[(int64_t)fj * cap + slot] = y * mw + x;
@@ -1167,7 +1181,15 @@ static int run_heat_tiled(const Src& src, const PostShape& s, PostBuffers& b, hi
   const int tx = (s.mw + kFT - 1) / kFT, ty = (s.mh + kFT - 1) / kFT;
   const int xm = s.n >= 8;
   const dim3 g((unsigned)((xm ? 8 * ((s.n + 7) / 8) : s.n) * tx * ty * OP_N_JOINTS));
-  if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
+  if (Src::kLow && s.peak_mode == OP_PEAKS_GPU_BRANCH) {  // op_set_peak_mode: the reference's GPU branch
+    const double* wg = b.gauss_w + kGaussGpuOff;
+    if (s.gpu_radius == 8)  // ksize 17, the reference's default
+      hipLaunchKernelGGL((heat_fused<Src, 8, Src::kLow>), g, dim3(kFN), 0, st, src, s.mh, s.mw, wg, s.gpu_radius,
+                         s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty, xm);
+    else
+      hipLaunchKernelGGL((heat_fused<Src, 0, Src::kLow>), g, dim3(kFN), 0, st, src, s.mh, s.mw, wg, s.gpu_radius,
+                         s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty, xm);
+  } else if (s.radius == 10)  // gaussian_sigma 2.5, the reference's default
     hipLaunchKernelGGL((heat_fused<Src, 10>), g, dim3(kFN), 0, st, src, s.mh, s.mw, b.gauss_w, s.radius,
                        s.peak_thresh, b.maxp, b.stage_key, b.stage_score, b.peak_cnt, s.n, tx, ty, xm);
   else
@@ -1216,7 +1238,7 @@ static inline unsigned pair_blocks(const PostBuffers& b) { return big_mode(b) ? 
 
 static int check_shape(const PostShape& s, const PostBuffers& b) {
   if (s.mw > 0xffff || s.mh > 0x7fff || s.n_integ > 16 || s.n_integ < 2 || (b.maxp > 2048 && !big_mode(b)) ||
-      s.radius > kMaxR ||
+      s.radius > kMaxR || (s.peak_mode && (s.gpu_radius > kMaxR || s.mh <= s.gpu_radius || s.mw <= s.gpu_radius)) ||
       s.mh <= s.radius || s.mw <= s.radius || (int64_t)s.mh * s.mw >= 0x7fffffff) {
     set_error("post-process shape outside kernel limits");
     return OP_ERR_INVALID;

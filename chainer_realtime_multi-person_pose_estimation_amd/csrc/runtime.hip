@@ -317,6 +317,11 @@ struct op_ctx {
   int pn = 0, pmh = 0, pmw = 0;  // post geometry
   std::vector<double> gauss_host;
   int gauss_r = 0;
+  // op_set_peak_mode: 1 = the reference's GPU-branch peaks (ksize x ksize unnormalised Gaussian,
+  // zero padding, >= NMS) in the single-scale post-process; gpu_taps = its 1-D factor (2 gpu_r + 1)
+  int peak_mode = 0;
+  int gpu_r = 0;
+  std::vector<double> gpu_taps;
   // staging
   uint8_t* d_frames = nullptr;
   size_t frames_bytes = 0;
@@ -479,6 +484,15 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
   return OP_OK;
 }
 
+// The device Gaussian table (PostBuffers::gauss_w): the CPU-branch taps (scipy's normalised 2r + 1)
+// at 0, the GPU-branch 1-D factor (op_set_peak_mode) at kGaussGpuOff
+static std::vector<double> gauss_table(const op_ctx* c) {
+  std::vector<double> t(op::kGaussTable, 0.0);
+  std::copy(c->gauss_host.begin(), c->gauss_host.end(), t.begin());
+  std::copy(c->gpu_taps.begin(), c->gpu_taps.end(), t.begin() + op::kGaussGpuOff);
+  return t;
+}
+
 static int ensure_post(op_ctx* c, int n, int mh, int mw) {
   if (c->pn >= n && c->pmh * c->pmw >= mh * mw && c->pb.up) return OP_OK;
   const int nn = std::max(n, c->pn), area = std::max(mh * mw, c->pmh * c->pmw);
@@ -511,7 +525,7 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
       {(void**)&b.res_scores, (size_t)nn * b.maxs * 8},
       {(void**)&b.res_subsets, (size_t)nn * b.maxs * 20 * 8},
       {(void**)&b.res_hdr, (size_t)nn * 4 * 4},
-      {(void**)&b.gauss_w, 64 * 8},
+      {(void**)&b.gauss_w, op::kGaussTable * 8},
   };
   static const char* const part_name[] = {"up",       "peak_xy",    "peak_score",
                                           "peak_cnt", "stage_key", "stage_score", "cand_score", "cand_idx",
@@ -537,7 +551,8 @@ static int ensure_post(op_ctx* c, int n, int mh, int mw) {
     p += g_guard;
   }
   OP_HIP_CHECK(hipDeviceSynchronize());
-  OP_HIP_CHECK(hipMemcpy(b.gauss_w, c->gauss_host.data(), c->gauss_host.size() * 8, hipMemcpyHostToDevice));
+  const std::vector<double> gt = gauss_table(c);
+  OP_HIP_CHECK(hipMemcpy(b.gauss_w, gt.data(), gt.size() * 8, hipMemcpyHostToDevice));
   c->pb = b;
   c->pn = nn;
   c->pmh = mh;
@@ -986,6 +1001,8 @@ static void post_shape(op_ctx* c, PostShape& s, int n, int lh, int lw, int mh, i
   s.mh = mh;
   s.mw = mw;
   s.radius = c->gauss_r;
+  s.peak_mode = c->peak_mode;
+  s.gpu_radius = c->gpu_r;
   s.img_len = img_len;
   s.sx = sx;
   s.sy = sy;
@@ -1058,7 +1075,7 @@ static int big_buffers(op_ctx* c, int maxp, int64_t maxc, PostBuffers** out) {
       {(void**)&b.conn_cnt, OP_N_LIMBS * 4},       {(void**)&b.sub_ids, S * OP_N_JOINTS * 4},
       {(void**)&b.sub_sc, S * 2 * 8},              {(void**)&b.res_poses, S * OP_N_JOINTS * 3 * 8},
       {(void**)&b.res_scores, S * 8},              {(void**)&b.res_subsets, S * 20 * 8},
-      {(void**)&b.res_hdr, 4 * 4},                 {(void**)&b.gauss_w, 64 * 8},
+      {(void**)&b.res_hdr, 4 * 4},                 {(void**)&b.gauss_w, op::kGaussTable * 8},
       {(void**)&b.used, OP_N_LIMBS * 2 * words * 4},
   };
   size_t total = 0;
@@ -1080,7 +1097,8 @@ static int big_buffers(op_ctx* c, int maxp, int64_t maxc, PostBuffers** out) {
     *q.p = p;
     p += (q.bytes + 255) / 256 * 256;
   }
-  OP_HIP_CHECK(hipMemcpy(b.gauss_w, c->pb.gauss_w, 64 * 8, hipMemcpyDeviceToDevice));
+  const std::vector<double> gt = gauss_table(c);
+  OP_HIP_CHECK(hipMemcpy(b.gauss_w, gt.data(), gt.size() * 8, hipMemcpyHostToDevice));
   c->bigb = b;
   *out = &c->bigb;
   return OP_OK;
@@ -3221,6 +3239,35 @@ int op_set_batch_invariant(op_ctx* c, int32_t enable) {
     c->gexec = nullptr;
   }
   c->splitk = sk;
+  return OP_OK;
+}
+
+int op_set_peak_mode(op_ctx* c, int32_t mode, int32_t ksize) {
+  using namespace op;
+  RC(check_ctx(c, false));
+  if (mode != OP_PEAKS_CPU_BRANCH && mode != OP_PEAKS_GPU_BRANCH) {
+    set_error("op_set_peak_mode: mode must be OP_PEAKS_CPU_BRANCH or OP_PEAKS_GPU_BRANCH");
+    return OP_ERR_INVALID;
+  }
+  if (mode == OP_PEAKS_GPU_BRANCH && (ksize < 3 || ksize > 2 * kMaxGaussR + 1 || (ksize & 1) == 0)) {
+    set_error("op_set_peak_mode: ksize must be odd, 3 .. " + std::to_string(2 * kMaxGaussR + 1));
+    return OP_ERR_INVALID;
+  }
+  OP_HIP_CHECK(hipStreamSynchronize(c->stream));
+  c->peak_mode = mode;
+  if (mode == OP_PEAKS_GPU_BRANCH) {
+    c->gpu_r = gpu_branch_taps(c->prm.gaussian_sigma, ksize, c->gpu_taps);
+  } else {
+    c->gpu_r = 0;
+    c->gpu_taps.clear();
+  }
+  const std::vector<double> gt = gauss_table(c);
+  for (PostBuffers* b : {&c->pb, &c->bigb})
+    if (b->gauss_w) OP_HIP_CHECK(hipMemcpy(b->gauss_w, gt.data(), gt.size() * 8, hipMemcpyHostToDevice));
+  if (c->gexec) {  // captured launches bake in the peak kernel
+    hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
   return OP_OK;
 }
 

@@ -29,10 +29,16 @@ class PoseDetector(object):
     batch_invariant: keep one accumulation order for every batch size (by default a lone frame's
                convolutions split their input channels over workgroups: ~2x lower latency, f32
                re-association ~1e-5 against the same frame in a batch).
+    peak_branch: which of the reference's two compute_peaks_from_heatmaps branches ``__call__``
+               follows: 'cpu' (default; pose_detector.py:82-110, scipy gaussian_filter + strict NMS,
+               what a reference detector with device=-1 returns) or 'gpu' (pose_detector.py:111-132,
+               the 17x17 unnormalised zero-padded Gaussian + >= NMS a reference detector built with
+               device >= 0 runs).  ``detect_precise`` and ``compute_peaks_from_heatmaps`` take the
+               CPU branch either way, as in the reference (NumPy heatmaps there).
     """
 
     def __init__(self, arch=None, weights_file=None, model=None, device=-1, precise=False, max_batch=1,
-                 precision="bf16x3", batch_invariant=False):
+                 precision="bf16x3", batch_invariant=False, peak_branch="cpu"):
         self.arch = arch
         self.precise = precise
         if model is None and arch not in (None, "posenet"):
@@ -44,6 +50,8 @@ class PoseDetector(object):
         self._ctx.set_precision(precision)
         if batch_invariant:  # one accumulation order for every batch size (op_set_batch_invariant)
             self._ctx.set_batch_invariant(True)
+        if peak_branch != "cpu":  # the reference's GPU-branch peaks in __call__ (op_set_peak_mode)
+            self._ctx.set_peak_mode(peak_branch, params["ksize"])
         if model is not None:
             w = model
         elif weights_file:

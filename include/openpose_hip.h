@@ -129,6 +129,19 @@ int op_set_stage_layout(op_ctx* ctx, int32_t planar);
  * near-threshold peaks of noisy maps can flip).  enable != 0 keeps one accumulation order for
  * every batch size (single-frame latency ~2x). */
 int op_set_batch_invariant(op_ctx* ctx, int32_t enable);
+/* Peak semantics of the single-scale post-process (op_detect, op_postprocess, op_run_staged*).
+ * The reference's compute_peaks_from_heatmaps has two branches and takes the one of the array it
+ * is handed: the CPU branch (pose_detector.py:82-110: scipy gaussian_filter sigma 2.5, reflect
+ * boundary, normalised 21 taps; strict > 4-neighbour NMS) for a CPU detector, the GPU branch
+ * (:111-132: F.convolution_2d with the ksize x ksize kernel of create_gaussian_kernel :38-44 --
+ * exp(-d^2 / 2 sigma^2) / (2 pi sigma^2), not normalised -- zero padding ksize/2; >= NMS) in
+ * __call__ of a detector built with device >= 0 (:29-35, :496-508).  OP_PEAKS_CPU_BRANCH (0, the
+ * default and the parity target of the golden fixtures) or OP_PEAKS_GPU_BRANCH (1; ksize odd,
+ * 3 .. 33, entity.py's 'ksize' is 17).  op_detect_precise and op_compute_peaks keep the CPU branch in
+ * either mode, as the reference does: their heatmaps are NumPy arrays there (:470-475). */
+#define OP_PEAKS_CPU_BRANCH 0
+#define OP_PEAKS_GPU_BRANCH 1
+int op_set_peak_mode(op_ctx* ctx, int32_t mode, int32_t ksize);
 
 /* serializers.load_npz(weights_file, model) (pose_detector.py:26): 92 layers in op_layer_info
  * order, W as Chainer (Co, Ci, k, k) f32 and b as (Co,) f32.  Packed into the kernel layout

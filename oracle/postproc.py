@@ -122,6 +122,51 @@ def compute_peaks_from_heatmaps(heatmaps, params=PARAMS):
     return out[:n].copy()
 
 
+def create_gaussian_kernel(sigma=1, ksize=5):
+    """pose_detector.py:38-44: the GPU branch's ksize x ksize kernel, exp(-d^2 / 2 sigma^2) /
+    (2 pi sigma^2) in f64, NOT normalised, stored as f32."""
+    center = int(ksize / 2)
+    grid_x = np.tile(np.arange(ksize), (ksize, 1))
+    grid_y = grid_x.transpose().copy()
+    grid_d2 = (grid_x - center) ** 2 + (grid_y - center) ** 2
+    return (1 / (sigma ** 2 * 2 * np.pi) * np.exp(-0.5 * grid_d2 / sigma ** 2)).astype("f")
+
+
+def gpu_branch_filter(heatmaps, params=PARAMS):
+    """pose_detector.py:112-113: F.convolution_2d(heatmaps[:, None], kernel, stride 1, pad ksize // 2)
+    of the (J, H, W) f32 maps, zero padding.  The reference runs it as a cuDNN f32 convolution whose
+    accumulation order is not specified; restated here as the exact sum (f64 over the f32 kernel)
+    rounded once to f32, so a correct device result lies within a few f32 ulp of it."""
+    h = np.asarray(heatmaps, np.float32)
+    k = create_gaussian_kernel(params["gaussian_sigma"], params["ksize"]).astype(np.float64)
+    ks = k.shape[0]
+    r = ks // 2
+    J, H, W = h.shape
+    pad = np.zeros((J, H + 2 * r, W + 2 * r), np.float64)
+    pad[:, r:r + H, r:r + W] = h
+    acc = np.zeros((J, H, W), np.float64)
+    for dy in range(ks):
+        for dx in range(ks):
+            acc += k[dy, dx] * pad[:, dy:dy + H, dx:dx + W]
+    return acc.astype(np.float32)
+
+
+def compute_peaks_gpu_branch(heatmaps, params=PARAMS):
+    """pose_detector.py:75-79, 111-132 (GPU branch): the background channel dropped, the filter
+    above, a peak where value > heatmap_peak_thresh and >= each of its 4 neighbours (0 outside the
+    map); rows [joint, x, y, score, id] f64 in (joint, y, x) order, ids consecutive."""
+    f = gpu_branch_filter(np.asarray(heatmaps)[:-1], params)
+    nb = np.zeros((4,) + f.shape, np.float32)
+    nb[0][:, 1:, :] = f[:, :-1, :]
+    nb[1][:, :-1, :] = f[:, 1:, :]
+    nb[2][:, :, 1:] = f[:, :, :-1]
+    nb[3][:, :, :-1] = f[:, :, 1:]
+    binary = (f > np.float32(params["heatmap_peak_thresh"])) & np.all(f[None] >= nb, axis=0)
+    c, y, x = np.nonzero(binary)
+    all_peaks = np.vstack((c, x, y, f[c, y, x])).transpose()
+    return np.hstack((all_peaks, np.arange(len(all_peaks)).reshape(-1, 1)))
+
+
 def compute_candidate_connections(paf, cand_a, cand_b, img_len, params=PARAMS):
     """pose_detector.py:135-159: list of [id_a, id_b, score] sorted by score desc."""
     paf = np.ascontiguousarray(paf, dtype=np.float32)
@@ -191,12 +236,16 @@ def subsets_to_pose_array(subsets, all_peaks):
     return np.array(person_pose_array)
 
 
-def postprocess(paf_low, heat_low, orig_h, orig_w, params=PARAMS, return_debug=False):
-    """pose_detector.py:501-517 from the last-stage network maps (38,h,w) and (19,h,w)."""
+def postprocess(paf_low, heat_low, orig_h, orig_w, params=PARAMS, return_debug=False, branch="cpu"):
+    """pose_detector.py:501-517 from the last-stage network maps (38,h,w) and (19,h,w); branch 'gpu':
+    the peaks of a detector built with device >= 0 (compute_peaks_gpu_branch)."""
     map_w, map_h = cvresize.compute_optimal_size(orig_h, orig_w, params["heatmap_size"])
     pafs = resize_images(paf_low, map_h, map_w)
     heatmaps = resize_images(heat_low, map_h, map_w)
-    all_peaks = compute_peaks_from_heatmaps(heatmaps, params)
+    if branch == "gpu":
+        all_peaks = compute_peaks_gpu_branch(heatmaps, params)
+    else:
+        all_peaks = compute_peaks_from_heatmaps(heatmaps, params)
     if len(all_peaks) == 0:
         res = (np.empty((0, N_JOINTS, 3)), np.empty(0))
         return (res + ({"all_peaks": all_peaks, "connections": None, "subsets": None},)) if return_debug else res
