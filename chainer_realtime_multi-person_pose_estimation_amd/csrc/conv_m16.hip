@@ -16,6 +16,12 @@
 #define M16_STAG_RING 6
 #endif
 static_assert(M16_STAG_RING == 6 || M16_STAG_RING == 4, "staggered ring: 4 or 6 taps");
+// M16_PF_L2 (round 6, A/B): waves 4-7 (the staggered half that stages no weights) pull chunk c + 1's
+// halo lines into L2 during pairs kPfPair .. kPfPair + 3 of chunk c, by 4-byte LDS-DMAs into a
+// spare KiB of their plane (nh < 28), so the chunk-boundary DMA reads L2 instead of MALL / HBM.
+#ifndef M16_PF_L2
+#define M16_PF_L2 0
+#endif
 
 namespace op {
 
@@ -27,7 +33,8 @@ namespace op {
 // fragment reads up to the first MFMA's issue), [3] pair loops incl. boundaries, [4] epilogue,
 // [5] pairs, [6] waves, [7] after the pair loop before the epilogue (final vmcnt wait); pair start
 // split: [8] the ring vmcnt wait, [9] the ring barrier, [10] the weight DMA issue
-__device__ unsigned long long g_m16_st[12];
+// [11] chunk boundaries' first barrier, [12] their halo DMA issue (the rest of [1]: DMA wait + barrier)
+__device__ unsigned long long g_m16_st[14];
 #define M16_T() __builtin_amdgcn_s_memtime()
 #endif
 
@@ -68,11 +75,15 @@ __device__ unsigned long long g_m16_st[12];
 // the staggered ring barriers then run on across chunk boundaries.  Tiles that cross a frame
 // border (two row sets, ~30 % at 640 px on 46 x 46 maps) or whose R3 would hold early rows keep
 // the drain.  Bit-identical: the same MFMAs on the same data in the same order.
-template <int KS, int NPX, bool DEEP = false, bool STAG = false, bool CIRC = false>
+// LIN (round 6): chunk-planar input whose halo pitch is the padded width (pad = R, the tight
+// pitch): a halo slot's source is one linear pixel index (a compare + select per piece where the
+// tile crosses a frame) instead of the row / column cursor with its per-piece carry loop.
+template <int KS, int NPX, bool DEEP = false, bool STAG = false, bool CIRC = false, bool LIN = false>
 __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
                                                           BigTiling tl) {
   static_assert(!STAG || M16_DMA_HALF, "staggered halves: waves 4-7 must not stage the ring");
   static_assert(!CIRC || (STAG && !DEEP && KS == 7), "circular halo: the staggered 7x7 ring kernel only");
+  static_assert(!LIN || (STAG && !DEEP && !CIRC), "linear halo sources: the staggered drained kernel");
   constexpr int KSQ = KS * KS;
   constexpr int R = KS / 2;
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
@@ -189,12 +200,29 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   const int h_r0 = h_sl0 / tl.pitch, h_c0 = h_sl0 - (h_sl0 / tl.pitch) * tl.pitch;
   // CIRC: this lane's row / column in piece 0 of a plane (the background cursor's start)
   const int hq_r0 = lane / tl.pitch, hq_c0 = lane - (lane / tl.pitch) * tl.pitch;
+  // LIN (the launcher checks chunk-planar input, pitch == padded width, pad == R): halo slot sl of
+  // the tile is linear pixel y0 * wp_in + sl of frame A's plane (sl < splitA), else pixel
+  // sl - splitA of frame B's
+  auto lin_src = [&](const char* a0, const char* b0, int sl, int splitA, int lastA) -> const char* {
+    return sl < splitA ? a0 + (int64_t)min(sl, lastA) * 16 : b0 + (int64_t)min(sl - splitA, hp_in * wp_in - 1) * 16;
+  };
   // this wave's pieces of chunk c's halo (LDS-DMA)
   auto issue_halo = [&](int c, const Tile& T) {
     const char* const fbase = (const char*)g.in + (int64_t)T.frame * hp_in * wp_in * pix_bytes;
     const char* const fbase_b = (const char*)g.in + (int64_t)T.fb * hp_in * wp_in * pix_bytes;
     const char* src0 = fbase + (int64_t)(c * 4 + h_plane) * in_pc;
     const char* src0_b = fbase_b + (int64_t)(c * 4 + h_plane) * in_pc;
+    if constexpr (LIN) {
+      const int splitA = T.rowsA < (1 << 29) ? T.rowsA * tl.pitch : (1 << 30);
+      const int lastA = (hp_in - T.y0) * wp_in - 1;
+      const char* const a0 = src0 + (int64_t)T.y0 * wp_in * 16;
+      char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
+      for (int i = h_i0; i < tl.nh; i += 2) {
+        glds16((const void*)lin_src(a0, src0_b, i * 64 + lane, splitA, lastA), dst);
+        dst += 2 * 1024;
+      }
+      return;
+    }
     int hr = h_r0, hc = h_c0;
     char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
     for (int i = h_i0; i < tl.nh; i += 2) {
@@ -295,7 +323,7 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 
     int it = cb0 * KSQP;
 #if M16_STAMPS
-    unsigned long long st_b = 0, st_p = 0, st_np = 0, st_v = 0, st_bar = 0, st_dma = 0;
+    unsigned long long st_b = 0, st_p = 0, st_np = 0, st_v = 0, st_bar = 0, st_dma = 0, st_b1 = 0, st_b2 = 0;
     const unsigned long long st_loop0 = M16_T();
 #endif
     for (int c = cb0; c < cb1; ++c) {
@@ -309,10 +337,22 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       if (!cont) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tb1 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #if M16_PROBE_NOHALO  // timing probe only (wrong results): the halo is loaded for the first chunk only
         if (c == cb0) issue_halo(c, T);
 #else
         issue_halo(c, T);
+#endif
+#if M16_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long tb2 = M16_T();
+        __builtin_amdgcn_sched_barrier(0);
+        st_b1 += tb1 - tb0;
+        st_b2 += tb2 - tb1;
 #endif
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
@@ -366,6 +406,25 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
 #endif
         stage_w(it + 2 * AHEAD);
         stage_w(it + 2 * AHEAD + 1);
+#if M16_PF_L2
+        if constexpr (LIN) {
+          constexpr int kPfPair = 8;
+          const int pk = (t >> 1) - kPfPair;
+          if (wave >= 4 && tl.nh < 28 && c + 1 < cb1 && pk >= 0 && pk * 64 * 8 < tl.nh * 64) {
+            // lane l: 128-B line pk * 64 + l of plane wave - 4 of chunk c + 1 (slots 8 apart)
+            const int pl = wave - 4;
+            const char* const pa = (const char*)g.in + (int64_t)T.frame * hp_in * wp_in * pix_bytes +
+                                   (int64_t)((c + 1) * 4 + pl) * in_pc;
+            const char* const pb0 = (const char*)g.in + (int64_t)T.fb * hp_in * wp_in * pix_bytes +
+                                    (int64_t)((c + 1) * 4 + pl) * in_pc;
+            const int splitA = T.rowsA < (1 << 29) ? T.rowsA * tl.pitch : (1 << 30);
+            const int sl = min((pk * 64 + lane) * 8, tl.nh * 64 - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const void*)lin_src(pa + (int64_t)T.y0 * wp_in * 16, pb0, sl, splitA, (hp_in - T.y0) * wp_in - 1),
+                (__attribute__((address_space(3))) void*)(halo + pl * HPLANE + 27 * 1024), 4, 0, 0);
+          }
+        }
+#endif
         if constexpr (CIRC) {
           if (circ && wave >= 4) {  // the background halo stream (see CIRC above), pair p = t / 2
             const int p = t >> 1;
@@ -525,6 +584,8 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       atomicAdd(&g_m16_st[8], st_v);
       atomicAdd(&g_m16_st[9], st_bar);
       atomicAdd(&g_m16_st[10], st_dma);
+      atomicAdd(&g_m16_st[11], st_b1);
+      atomicAdd(&g_m16_st[12], st_b2);
     }
 #endif
   }
@@ -552,7 +613,12 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 9, false, true, true>,
                          (const void*)conv_m16_bf16x3<7, 8, false, true, true>,
                          (const void*)conv_m16_bf16x3<7, 7, false, true, true>,
-                         (const void*)conv_m16_bf16x3<7, 6, false, true, true>};
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, true, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 9, false, true, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, true, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 7, false, true, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -586,8 +652,14 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   // (incremental staging cursor: 76.0 -> 80.4 ms, profiles/r06/ab_r06c_incr_scalar_cursor_not_kept.log)
   const char* circ_env = getenv("OP_M16_CIRC");
   const bool circ = stag && !deep && npx >= 6 && circ_env && atoi(circ_env) == 1;
+  // round 6: linear halo sources (LIN) on chunk-planar input with the tight pitch (OP_M16_LIN=1, read
+  // per call)
+  const char* lin_env = getenv("OP_M16_LIN");
+  const bool lin = stag && !deep && !circ && npx >= 6 && s.in_planar && s.pin == 3 && tl.pitch == s.w + 2 * s.pin &&
+                   lin_env && atoi(lin_env) == 1;
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_LAUNCH_C(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
+#define M16_LAUNCH_L(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_CASE(N)                                  \
   case N:                                            \
     if (deep && N <= 5) {                            \
@@ -595,6 +667,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
       else M16_LAUNCH(N, (N <= 5), false);           \
     } else if (stag) {                               \
       if (circ && N >= 6) M16_LAUNCH_C((N >= 6 ? N : 6)); \
+      else if (lin && N >= 6) M16_LAUNCH_L((N >= 6 ? N : 6)); \
       else M16_LAUNCH(N, false, true);               \
     } else {                                         \
       M16_LAUNCH(N, false, false);                   \
@@ -611,35 +684,39 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
     M16_CASE(2)
     default:
       if (circ) M16_LAUNCH_C(10);
+      else if (lin) M16_LAUNCH_L(10);
       else if (stag) M16_LAUNCH(10, false, true);
       else M16_LAUNCH(10, false, false);
   }
 #undef M16_CASE
 #undef M16_LAUNCH
 #undef M16_LAUNCH_C
+#undef M16_LAUNCH_L
   census_add(stag ? OP_CENSUS_7X7_STAG : OP_CENSUS_7X7_PLAIN_RING);
   if (circ) census_add(OP_CENSUS_7X7_CIRC);
+  if (lin) census_add(OP_CENSUS_7X7_LIN);
 #if M16_STAMPS
   static const bool dump = getenv("OP_M16_STAMPS") != nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (dump && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone && tl.ksplit == 1) {
-    static unsigned long long tot[12] = {};
+    static unsigned long long tot[14] = {};
     static int launches = 0;
-    unsigned long long h[12];
+    unsigned long long h[14];
     OP_HIP_CHECK(hipStreamSynchronize(st));
     OP_HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_m16_st), sizeof(h)));
-    const unsigned long long z[12] = {};
+    const unsigned long long z[14] = {};
     OP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_m16_st), z, sizeof(z)));
-    for (int i = 0; i < 12; ++i) tot[i] += h[i];
+    for (int i = 0; i < 14; ++i) tot[i] += h[i];
     if (++launches % 25 == 0) {
       const double w = (double)tot[0];
       fprintf(stderr,
               "M16_STAMPS npx %d launches %d waves %llu pairs/wave %.1f | per wave cycles %.0f | chunk boundary %.4f "
               "pair start %.4f (vmcnt %.4f barrier %.4f dma %.4f) pair loop %.4f (pure pairs %.4f) final wait %.4f "
-              "epilogue %.4f prologue %.4f\n",
+              "epilogue %.4f prologue %.4f | chunk boundary: first barrier %.4f halo issue %.4f\n",
               npx, launches, tot[6], (double)tot[5] / tot[6], w / tot[6], tot[1] / w, tot[2] / w, tot[8] / w, tot[9] / w,
               tot[10] / w, tot[3] / w,
-              (tot[3] - tot[1] - tot[2]) / w, tot[7] / w, tot[4] / w, (w - tot[3] - tot[7] - tot[4]) / w);
+              (tot[3] - tot[1] - tot[2]) / w, tot[7] / w, tot[4] / w, (w - tot[3] - tot[7] - tot[4]) / w, tot[11] / w,
+              tot[12] / w);
     }
   }
 #endif

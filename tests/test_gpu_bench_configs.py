@@ -379,6 +379,28 @@ def test_circular_halo_bit_identical(lib, bctx, monkeypatch, n):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
 
 
+@pytest.mark.parametrize("n", [38, 232])
+def test_linear_halo_sources_bit_identical(lib, bctx, monkeypatch, n):
+    """Round 6: the staggered 7x7 kernel with linear halo sources (conv_m16.hip LIN: on chunk-planar
+    input with the tight pitch a halo slot's source pixel is one linear index; OP_M16_LIN=0 keeps the
+    row / column cursor) loads the same pixels into the same LDS slots: the maps are bit-identical
+    at 38 frames and at the headline's 232, and the census shows LIN ran every 7x7 launch."""
+    rng = np.random.default_rng(500 + n)
+    x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
+    out = {}
+    for lin in ("1", "0"):
+        monkeypatch.setenv("OP_M16_LIN", lin)
+        _census_npx(lib)
+        out[lin] = bctx.forward(x)
+        cen = _census_npx(lib)
+        print("n %d OP_M16_LIN=%s census:" % (n, lin), cen)
+        assert cen["7x7_stag"] == 25, cen
+        assert cen["7x7_lin"] == (25 if lin == "1" else 0), cen
+    monkeypatch.delenv("OP_M16_LIN")
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
 def test_staggered_halves_precise_720p(lib, monkeypatch):
     """The staggered 7x7 halves on the multi-scale path's wide maps (41- to 164-column maps, halo
     planes up to 32 KiB, frame-aligned and tight-pitch raster tiles): 2 frames of 1280x720 through
