@@ -908,7 +908,11 @@ static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, in
   if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
   if (iwg) census_add(OP_CENSUS_7X7_Q_IWG);
-  const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t, iwg);
+  // round 6: B fragments one tap ahead (OP_M16Q_BPF=1, read per launch)
+  const char* bpf_env = getenv("OP_M16Q_BPF");
+  const bool bpf = !iwg && tr == 4 && nth == 2 && pfk == 2 && bpf_env && atoi(bpf_env) == 1;
+  if (bpf) census_add(OP_CENSUS_7X7_Q_BPF);
+  const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t, iwg, bpf);
   if (rc != OP_OK) return rc;
   OP_AFTER_LAUNCH("conv_m16q_bf16x3", st);
   const int64_t items = (int64_t)t.total * (cop_max / 4);

@@ -148,6 +148,6 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
 int launch_conv_m16w(const SplitConvShape& s, const SplitConvGroup* g, int cop_max, hipStream_t st, int* taken);
 int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                     const SplitConvGroup& g1, const BigTiling& tl,
-                    bool iwg);
+                    bool iwg, bool bpf);
 
 }  // namespace op

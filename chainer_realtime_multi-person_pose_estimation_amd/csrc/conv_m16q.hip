@@ -59,7 +59,11 @@ __device__ __forceinline__ void q_dma16(const void* gsrc, uint32_t lds_byte) {
 // (range 0 + range 1 + ..., exchanged through the halo's space) before the f32 partials are
 // written: the split-K index is the chunk pair alone, so the partials and the reduce launch that
 // reads them shrink NTH-fold (one frame's Mconv2-5: 8 -> 4 partials of 8.7 MB).
-template <int KS, int TR, int NTH, int PF, bool IWG = false>
+// BPF (round 6): the tap's B fragments (TR rows x hi / lo, 8 ds_read_b128 at TR 4) are read from LDS
+// one tap ahead into PF + 1 register sets, so a tap's MFMAs start on fragments that landed a whole
+// tap earlier; without it each tap waits for its own 8 LDS reads at its first MFMA and again for the
+// last two in its middle (the compiled loop: s_waitcnt lgkmcnt(0) before the first MFMA of a tap).
+template <int KS, int TR, int NTH, int PF, bool IWG = false, bool BPF = false>
 __global__ __launch_bounds__(IWG ? 256 * NTH : 256, 3) void conv_m16q_bf16x3(SplitConvShape s, SplitConvGroup g0,
                                                                             SplitConvGroup g1, BigTiling tl) {
   constexpr int KSQ = KS * KS, R = KS / 2;
@@ -154,19 +158,41 @@ __global__ __launch_bounds__(IWG ? 256 * NTH : 256, 3) void conv_m16q_bf16x3(Spl
 
   // this lane's slot in its (chunk csel, k-half khalf) hi plane; block pb = tile row pb
   const char* const hb = lds + (csel * 4 + 2 * khalf) * HPLANE + l16 * 16;
+  typedef bf16x8g BFrag[TR][2];  // [pb][hi, lo]
+  auto load_b = [&](int t, BFrag& b) {
+    if (t >= t1) t = t1 - 1;  // the last tap's prefetch re-reads the final tap (unused)
+    const int tr = t / KS, tc = t - (t / KS) * KS;
+    const char* const tb = hb + (tr * PITCH + tc) * 16;
+#pragma unroll
+    for (int pb = 0; pb < TR; ++pb) {
+      b[pb][0] = *(const bf16x8g*)(tb + pb * PITCH * 16);
+      b[pb][1] = *(const bf16x8g*)(tb + pb * PITCH * 16 + HPLANE);
+    }
+  };
+  BFrag bbuf[BPF ? 2 : 1];
+  if constexpr (BPF) load_b(t0, bbuf[0]);
   // one tap: the weights of tap t + PF into buffer (B + PF) % (PF + 1), then tap t's MFMAs from
-  // buffer B (B = the tap's index mod PF + 1, a compile-time constant)
-  auto step = [&](int t, auto bsel) {
-    constexpr int B = decltype(bsel)::value;
+  // buffer B (K = the tap's index mod G, a compile-time constant; B = K mod PF + 1; BPF: the B
+  // fragments of tap t + 1 into set (K + 1) mod 2, tap t's from set K mod 2)
+  auto step = [&](int t, auto ksel) {
+    constexpr int K = decltype(ksel)::value;
+    constexpr int B = K % (PF + 1), BB = K % 2;
     load_a(t + PF, abuf[(B + PF) % (PF + 1)]);
+    if constexpr (BPF) {
+      // this tap's fragments (issued a tap ago) have landed before the next tap's are issued: at
+      // most 8 LDS reads in flight (lgkmcnt is 4 bits); the builtin wait is visible to the
+      // compiler's counter, so the MFMAs below need no further LDS wait
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (vmcnt 63, expcnt 7: no wait on those)
+      load_b(t + 1, bbuf[BPF ? (BB + 1) % 2 : 0]);
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the step's start
     const int tr = t / KS, tc = t - (t / KS) * KS;
     const char* const tb = hb + (tr * PITCH + tc) * 16;
     const AFrag& a = abuf[B];
 #pragma unroll
     for (int pb = 0; pb < TR; ++pb) {
-      const bf16x8g bh = *(const bf16x8g*)(tb + pb * PITCH * 16);
-      const bf16x8g bl = *(const bf16x8g*)(tb + pb * PITCH * 16 + HPLANE);
+      const bf16x8g bh = BPF ? bbuf[BPF ? BB : 0][pb][0] : *(const bf16x8g*)(tb + pb * PITCH * 16);
+      const bf16x8g bl = BPF ? bbuf[BPF ? BB : 0][pb][1] : *(const bf16x8g*)(tb + pb * PITCH * 16 + HPLANE);
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb], bh, acc[cb][pb], 0, 0, 0);
@@ -174,29 +200,38 @@ __global__ __launch_bounds__(IWG ? 256 * NTH : 256, 3) void conv_m16q_bf16x3(Spl
         acc[cb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2 * cb + 1], bh, acc[cb][pb], 0, 0, 0);
       }
     }
+    if constexpr (BPF) __builtin_amdgcn_sched_barrier(0);  // the next tap's loads stay behind these MFMAs
   };
   // A rolled loop of PF + 1 taps per iteration (each buffer index compile-time, so the back-edge
   // carries the buffers in place), then the 0..PF remaining taps: 989 instead of 2248 lines of
   // code with every tap unrolled, the same time (profiles/r05/ab_r05u_b1_m16q_rolled.log).
-  constexpr int G = PF + 1;
+  // BPF: G = 2 (PF + 1) taps per iteration, so both the A and the B set indices are compile-time
+  constexpr int G = BPF ? 2 * (PF + 1) : PF + 1;
+  static_assert(G <= 6, "the unrolled iteration holds at most 6 taps");
   const int n = t1 - t0;
   const int ng = n / G;
   int t = t0;
+#define M16Q_STEP(k) step(t + (k), std::integral_constant<int, ((k) < G ? (k) : 0)>())
 #pragma unroll 1
   for (int i = 0; i < ng; ++i, t += G) {
-    step(t, std::integral_constant<int, 0>());
-    step(t + 1, std::integral_constant<int, 1>());
-    step(t + 2, std::integral_constant<int, 2>());
-    if constexpr (G > 3) step(t + 3, std::integral_constant<int, (G > 3 ? 3 : 0)>());
-    if constexpr (G > 4) step(t + 4, std::integral_constant<int, (G > 4 ? 4 : 0)>());
+    M16Q_STEP(0);
+    M16Q_STEP(1);
+    M16Q_STEP(2);
+    if constexpr (G > 3) M16Q_STEP(3);
+    if constexpr (G > 4) M16Q_STEP(4);
+    if constexpr (G > 5) M16Q_STEP(5);
   }
   const int rem = n - ng * G;
-  if (rem > 0) step(t, std::integral_constant<int, 0>());
-  if (rem > 1) step(t + 1, std::integral_constant<int, 1>());
+  if (rem > 0) M16Q_STEP(0);
+  if (rem > 1) M16Q_STEP(1);
   if constexpr (G > 3) {
-    if (rem > 2) step(t + 2, std::integral_constant<int, 2>());
-    if (rem > 3) step(t + 3, std::integral_constant<int, (G > 3 ? 3 : 0)>());
+    if (rem > 2) M16Q_STEP(2);
+    if (rem > 3) M16Q_STEP(3);
   }
+  if constexpr (G > 5) {
+    if (rem > 4) M16Q_STEP(4);
+  }
+#undef M16Q_STEP
 
 #if M16Q_STAMPS
   __builtin_amdgcn_sched_barrier(0);
@@ -260,7 +295,7 @@ __global__ __launch_bounds__(IWG ? 256 * NTH : 256, 3) void conv_m16q_bf16x3(Spl
 }
 
 int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
-                    const SplitConvGroup& g1, const BigTiling& tl, bool iwg) {
+                    const SplitConvGroup& g1, const BigTiling& tl, bool iwg, bool bpf) {
   // OP_M16Q_LDS_KB (A/B aid): allocate at least that much LDS per workgroup (caps workgroups per CU)
   static const int lds_min = getenv("OP_M16Q_LDS_KB") ? atoi(getenv("OP_M16Q_LDS_KB")) * 1024 : 0;
   auto lds_of = [](int r) { return std::max(lds_min, 8 * (((r + 6) * 22 + 63) / 64) * 1024); };
@@ -272,6 +307,13 @@ int launch_m16q_7x7(int tr, int nth, int pf, hipStream_t st, const SplitConvShap
       hipLaunchKernelGGL((conv_m16q_bf16x3<7, 4, 2, 2, true>), grid, dim3(512), lds_of(4), st, s, g0, g1, tl);
     } else {
       set_error("conv_m16q_bf16x3 (tap ranges in one workgroup): tile rows 4, 2 tap ranges, prefetch 2 only");
+      return OP_ERR_INVALID;
+    }
+  } else if (bpf) {  // B fragments one tap ahead (round 6): tile rows 4, prefetch 2, 2 tap ranges
+    if (tr == 4 && nth == 2 && pf == 2) {
+      hipLaunchKernelGGL((conv_m16q_bf16x3<7, 4, 2, 2, false, true>), grid, dim3(256), lds_of(4), st, s, g0, g1, tl);
+    } else {
+      set_error("conv_m16q_bf16x3 (B prefetch): tile rows 4, 2 tap ranges, prefetch 2 only");
       return OP_ERR_INVALID;
     }
   } else if (tr == 4 && (pf == 2 || pf == 4) && nth >= 2 && nth <= 4) {

@@ -74,6 +74,24 @@ def test_one_frame_vs_reference_fixture(lib, qctx, monkeypatch, tr, nth, pf, iwg
     assert e <= TOL, e
 
 
+def test_b_prefetch_bit_identical(lib, qctx, monkeypatch):
+    """Round 6 (OP_M16Q_BPF=1): the B fragments read one tap ahead into two register sets change when
+    each LDS read is issued, not the MFMAs or their order: the one-frame maps are bit-identical to
+    the default kernel's, within TOL of the reference fixture, and the census shows it ran every
+    7x7 launch."""
+    x, want_paf, want_heat = _fixture()
+    out = {}
+    for bpf in ("1", "0"):
+        monkeypatch.setenv("OP_M16Q_BPF", bpf)
+        lib.conv_census(reset=True)
+        out[bpf] = qctx.forward(x)
+        cen = lib.conv_census(reset=True)
+        assert cen["7x7_q"] == 25 and cen["7x7_q_bpf"] == (25 if bpf == "1" else 0), cen
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b), _max_err(a, b)
+    assert max(_max_err(out["1"][0][0], want_paf), _max_err(out["1"][1][0], want_heat)) <= TOL
+
+
 def test_vs_conv_m16_split_k_and_invariant_mode(lib, qctx, monkeypatch):
     x, _, _ = _fixture()
     lib.conv_census(reset=True)
