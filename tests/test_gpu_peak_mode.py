@@ -4,8 +4,9 @@ compute_peaks_gpu_branch).
 
 Parity unpinned against the reference itself (its GPU branch needs CUDA + cuDNN, so no fixture of
 it exists).  The device filter is separable f64 with one f32 rounding between the passes; the oracle
-is the exact 2-D sum rounded once.  Tolerance: peak sets and poses exact (the golden maps have no
-decision within 1e-4 of a tie, asserted below), scores within 1e-6 relative."""
+is the exact 2-D sum rounded once.  Tolerance: peak sets and poses exact (no peak decision of the
+inputs lies within 5e-7 of a tie relative to the map maximum, asserted below), scores within 1e-6
+relative."""
 import numpy as np
 import pytest
 
@@ -26,20 +27,22 @@ def gctx(lib, rand_weights):
 
 
 def _decision_margin(heat_low, orig_h, orig_w):
-    """Smallest gap, relative to the map maximum, between a filtered value above the threshold and
-    the threshold or one of its 4 neighbours: the room a rounding difference has before a peak flips."""
+    """Relative room a rounding difference has before one peak decision flips: for a peak, its
+    smallest gap to the threshold or a neighbour; for any other pixel, its largest failing gap (all
+    of them must flip to make it a peak).  Neighbours outside the map count as 0."""
     from oracle import cvresize
     mw, mh = cvresize.compute_optimal_size(orig_h, orig_w, 320)
     f = P.gpu_branch_filter(P.resize_images(heat_low, mh, mw)[:-1]).astype(np.float64)
-    live = f > 0.05 - 1e-3
-    if not live.any():
-        return np.inf
-    gaps = [np.abs(f - 0.05)]
-    for sh in ((1, 0), (-1, 0), (0, 1), (0, -1)):
-        g = np.abs(f - np.roll(f, sh, axis=(1, 2)))
-        gaps.append(g)
-    m = min(float(g[live].min()) for g in gaps)
-    return m / max(float(f.max()), 1e-30)
+    pad = np.pad(f, ((0, 0), (1, 1), (1, 1)))
+    g = [f - np.float64(np.float32(0.05))]
+    for dy, dx in ((0, 1), (2, 1), (1, 0), (1, 2)):
+        g.append(f - pad[:, dy:dy + f.shape[1], dx:dx + f.shape[2]])
+    g = np.stack(g)
+    peak = (g[0] > 0) & np.all(g[1:] >= 0, axis=0)
+    m_peak = np.where(peak, np.abs(g).min(axis=0), np.inf)
+    fail = np.where(np.concatenate([(g[0] <= 0)[None], g[1:] < 0]), np.abs(g), 0.0)
+    m_non = np.where(~peak, fail.max(axis=0), np.inf)
+    return min(float(m_peak.min()), float(m_non.min())) / max(float(f.max()), 1e-30)
 
 
 @pytest.mark.parametrize("case", golden_cases())
@@ -48,7 +51,9 @@ def test_gpu_branch_postprocess_vs_oracle(gctx, case):
     oh, ow = int(d["orig_h"]), int(d["orig_w"])
     poses, scores, res = gctx.postprocess(d["paf_low"], d["heat_low"], oh, ow)
     want_p, want_s, dbg = P.postprocess(d["paf_low"], d["heat_low"], oh, ow, return_debug=True, branch="gpu")
-    assert _decision_margin(d["heat_low"], oh, ow) > 1e-4  # no near-tie the rounding could flip
+    # no decision within ~7 f32 ulp of a tie (the golden maps' closest is 7.5e-7, noise_crowd), where
+    # the device's two-pass rounding (~1e-7) could flip it
+    assert _decision_margin(d["heat_low"], oh, ow) > 5e-7
     assert res.n_peaks == len(dbg["all_peaks"])
     assert res.n_persons == len(want_s)
     if len(want_s):
@@ -109,6 +114,7 @@ def test_pose_detector_gpu_branch_equals_oracle_composition(pkg, rand_weights):
     x = det._ctx.preprocess(img, 368, 368)
     paf, heat = det._ctx.forward(x)
     want_p, want_s = P.postprocess(paf[0], heat[0], img.shape[0], img.shape[1], branch="gpu")
+    assert _decision_margin(heat[0], img.shape[0], img.shape[1]) > 5e-7
     poses, scores = det(img)
     assert np.asarray(poses).shape == np.asarray(want_p).shape
     if len(want_s):
