@@ -53,8 +53,9 @@ def _fixture():
                                            ("8", "2", "2", "1"), ("4", "3", "2", "1"), ("4", "4", "2", "1"),
                                            ("4", "2", "4", "1")])
 def test_one_frame_vs_reference_fixture(lib, qctx, monkeypatch, tr, nth, pf, iwg):
-    """Every instantiation, incl. round 6's default (TR 4, 2 tap ranges in one 8-wave workgroup,
-    iwg 1) and round 5's one workgroup per (chunk pair, tap range) (iwg 0)."""
+    """Every instantiation, incl. round 6's opt-in in-workgroup tap ranges (TR 4, 2 tap ranges in one
+    8-wave workgroup, iwg 1; measured slower, OP_M16Q_IWG=1) and the default one workgroup per (chunk
+    pair, tap range) (iwg 0)."""
     monkeypatch.setenv("OP_M16Q_TR", tr)
     monkeypatch.setenv("OP_M16Q_NTH", nth)
     monkeypatch.setenv("OP_M16Q_PF", pf)
