@@ -55,3 +55,44 @@ def test_peak_rows_order_and_ids():
     assert np.all(np.diff(key) > 0)
     assert np.array_equal(g[:, 4], np.arange(len(g)))
     assert np.all(g[:, 3] > 0.05)
+
+
+def _separable_like_the_device(h, sigma=2.5, ksize=17):
+    """The device's arithmetic for the GPU branch (postproc.hip heat_fused<.., G>): the 1-D factor
+    g(d) = exp(-d^2 / 2 s^2) / sqrt(2 pi s^2) (host_pack.hpp gpu_branch_taps), a vertical then a
+    horizontal pass in f64 over zero-padded f32 maps, rounded to f32 after each pass."""
+    r = ksize // 2
+    d = np.arange(-r, r + 1, dtype=np.float64)
+    g = np.exp(-0.5 * d * d / (sigma * sigma)) / np.sqrt(2.0 * np.pi * sigma * sigma)
+    J, H, W = h.shape
+    p = np.zeros((J, H + 2 * r, W), np.float64)
+    p[:, r:r + H] = h
+    v = sum(g[k] * p[:, k:k + H] for k in range(ksize)).astype(np.float32)
+    q = np.zeros((J, H, W + 2 * r), np.float64)
+    q[:, :, r:r + W] = v
+    return sum(g[k] * q[:, :, k:k + W] for k in range(ksize)).astype(np.float32)
+
+
+def test_device_arithmetic_within_rounding_of_the_restatement():
+    """The separable f64 / f32-between-passes form the device runs stays within a few f32 ulp of the
+    oracle's exact 2-D sum on the golden maps (upsampled like the single-scale path)."""
+    from conftest import golden_cases, load_golden
+    from oracle import cvresize
+    for case in golden_cases():
+        d = load_golden(case)
+        mw, mh = cvresize.compute_optimal_size(int(d["orig_h"]), int(d["orig_w"]), 320)
+        heat = P.resize_images(d["heat_low"], mh, mw)[:-1]
+        a = P.gpu_branch_filter(heat).astype(np.float64)
+        b = _separable_like_the_device(heat).astype(np.float64)
+        scale = max(float(np.abs(a).max()), 1e-30)
+        assert float(np.abs(a - b).max()) <= 3e-7 * scale, case
+        # ... and finds the same peaks
+        want = P.compute_peaks_gpu_branch(np.concatenate([heat, heat[:1]]))
+        nb = np.zeros((4,) + b.shape, np.float32)
+        bf = b.astype(np.float32)
+        nb[0][:, 1:, :] = bf[:, :-1, :]
+        nb[1][:, :-1, :] = bf[:, 1:, :]
+        nb[2][:, :, 1:] = bf[:, :, :-1]
+        nb[3][:, :, :-1] = bf[:, :, 1:]
+        got = np.argwhere((bf > np.float32(0.05)) & np.all(bf[None] >= nb, axis=0))
+        assert np.array_equal(got[:, [0, 2, 1]].astype(np.float64), want[:, :3].reshape(-1, 3)), case
