@@ -487,9 +487,13 @@ static int ensure_geometry(op_ctx* c, int n, int h, int w) {
 // The device Gaussian table (PostBuffers::gauss_w): the CPU-branch taps (scipy's normalised 2r + 1)
 // at 0, the GPU-branch 1-D factor (op_set_peak_mode) at kGaussGpuOff
 static std::vector<double> gauss_table(const op_ctx* c) {
+  // (a sigma whose radius passes kMaxR -- 2r + 1 > 33 taps -- is refused by check_shape before any
+  // launch; its table is cut at the region's end rather than written past it)
   std::vector<double> t(op::kGaussTable, 0.0);
-  std::copy(c->gauss_host.begin(), c->gauss_host.end(), t.begin());
-  std::copy(c->gpu_taps.begin(), c->gpu_taps.end(), t.begin() + op::kGaussGpuOff);
+  const size_t nc = std::min<size_t>(c->gauss_host.size(), op::kGaussGpuOff);
+  const size_t ng = std::min<size_t>(c->gpu_taps.size(), op::kGaussTable - op::kGaussGpuOff);
+  std::copy(c->gauss_host.begin(), c->gauss_host.begin() + nc, t.begin());
+  std::copy(c->gpu_taps.begin(), c->gpu_taps.begin() + ng, t.begin() + op::kGaussGpuOff);
   return t;
 }
 
