@@ -1070,6 +1070,9 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         tl.pair = 1;
       }
       tl.zeros = device_zeros();
+      // round 6: LIN tiles within one frame load only their own halo rows (OP_M16_TRIM, read per launch)
+      const char* trim_env = getenv("OP_M16_TRIM");
+      tl.halo_trim = trim_env && atoi(trim_env) == 1;
       if (!tl.zeros) {
         set_error("conv_m16_bf16x3: conv_big_device_init was not called for this device");
         return OP_ERR_STATE;

@@ -30,6 +30,7 @@ struct BigTiling {
   int32_t ksplit;            // > 1 (conv_m16): input chunks split over blockIdx.y, f32 partials in ws
   float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
   const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
+  int32_t halo_trim;         // conv_m16 LIN: a tile within one frame loads only its own halo rows' pieces
 };
 
 template <int N>

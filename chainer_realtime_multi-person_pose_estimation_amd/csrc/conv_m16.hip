@@ -217,7 +217,15 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
       const int lastA = (hp_in - T.y0) * wp_in - 1;
       const char* const a0 = src0 + (int64_t)T.y0 * wp_in * 16;
       char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
-      for (int i = h_i0; i < tl.nh; i += 2) {
+      // halo_trim: a tile within one frame reads halo slots < its rows x pitch only (its output rows +
+      // 2R; block q = (y - y0) * pitch + x plus tap offsets < 2R * pitch + 2R): the pieces past them
+      // (the plane is sized for the frame-crossing tiles' extra 2R rows) are not loaded
+      int np = tl.nh;
+      if (tl.halo_trim && T.fb == T.frame) {
+        const int rows = (T.P1 - T.frame * tl.hw) / s.w - T.y0 + 1 + 2 * R;
+        np = min(np, (rows * tl.pitch + 63) / 64);
+      }
+      for (int i = h_i0; i < np; i += 2) {
         glds16((const void*)lin_src(a0, src0_b, i * 64 + lane, splitA, lastA), dst);
         dst += 2 * 1024;
       }

@@ -388,17 +388,20 @@ def test_linear_halo_sources_bit_identical(lib, bctx, monkeypatch, n):
     rng = np.random.default_rng(500 + n)
     x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
     out = {}
-    for lin in ("1", "0"):
+    for lin, trim in (("1", "1"), ("1", "0"), ("0", "0")):  # trim: only a tile's own halo rows loaded
         monkeypatch.setenv("OP_M16_LIN", lin)
+        monkeypatch.setenv("OP_M16_TRIM", trim)
         _census_npx(lib)
-        out[lin] = bctx.forward(x)
+        out[lin + trim] = bctx.forward(x)
         cen = _census_npx(lib)
-        print("n %d OP_M16_LIN=%s census:" % (n, lin), cen)
+        print("n %d OP_M16_LIN=%s OP_M16_TRIM=%s census:" % (n, lin, trim), cen)
         assert cen["7x7_stag"] == 25, cen
         assert cen["7x7_lin"] == (25 if lin == "1" else 0), cen
     monkeypatch.delenv("OP_M16_LIN")
-    for a, b in zip(out["1"], out["0"]):
-        assert np.array_equal(a, b), float(np.abs(a - b).max())
+    monkeypatch.delenv("OP_M16_TRIM")
+    for k in ("11", "10"):
+        for a, b in zip(out[k], out["00"]):
+            assert np.array_equal(a, b), (k, float(np.abs(a - b).max()))
 
 
 def test_staggered_halves_precise_720p(lib, monkeypatch):
