@@ -281,7 +281,7 @@ CENSUS = {"7x7_splitk": 11, "7x7_other": 12, "3x3_w48": 13, "3x3_w32": 14, "3x3_
           "7x7_planar": 22, "7x7_frame_aligned": 23, "7x7_tight": 24,
           "cubic_fused": 25, "cubic_two_pass": 26,
           "cubic_rows": 28, "f32_lds": 29, "7x7_stag": 30, "7x7_plain_ring": 31,
-          "7x7_q": 32, "7x7_circ": 33, "precise_side": 34, "7x7_q_iwg": 35, "7x7_lin": 36, "7x7_q_bpf": 37}
+          "7x7_q": 32, "7x7_circ": 33, "precise_side": 34, "7x7_q_iwg": 35, "7x7_lin": 36, "7x7_q_bpf": 37, "7x7_pers": 38}
 CENSUS_SLOTS = 40
 
 

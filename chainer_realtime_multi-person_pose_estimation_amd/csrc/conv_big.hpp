@@ -31,6 +31,7 @@ struct BigTiling {
   float* ws;                 // ksplit partials [split][group][pixel][cop] (conv_m16_splitk_reduce)
   const void* zeros;         // conv_m16: >= 1 KiB of device zeros (the padding tap of an odd tap count)
   int32_t halo_trim;         // conv_m16 LIN: a tile within one frame loads only its own halo rows' pieces
+  int32_t pers_blocks;       // conv_m16 PERS: the launch's tile count (the grid is one workgroup per CU)
 };
 
 template <int N>

@@ -78,9 +78,10 @@ __device__ unsigned long long g_m16_st[14];
 // LIN (round 6): chunk-planar input whose halo pitch is the padded width (pad = R, the tight
 // pitch): a halo slot's source is one linear pixel index (a compare + select per piece where the
 // tile crosses a frame) instead of the row / column cursor with its per-piece carry loop.
-template <int KS, int NPX, bool DEEP = false, bool STAG = false, bool CIRC = false, bool LIN = false>
-__global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
-                                                          BigTiling tl) {
+// One tile (block id lin) of the launch; the kernel below runs one, or (PERS) a loop of them.
+template <int KS, int NPX, bool DEEP, bool STAG, bool CIRC, bool LIN>
+__device__ __forceinline__ void m16_tile(const SplitConvShape& s, const SplitConvGroup& g0, const SplitConvGroup& g1,
+                                         const BigTiling& tl, const int lin) {
   static_assert(!STAG || M16_DMA_HALF, "staggered halves: waves 4-7 must not stage the ring");
   static_assert(!CIRC || (STAG && !DEEP && KS == 7), "circular halo: the staggered 7x7 ring kernel only");
   static_assert(!LIN || (STAG && !DEEP && !CIRC), "linear halo sources: the staggered drained kernel");
@@ -98,7 +99,6 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   constexpr int HPLANE = (DEEP ? 16 : (STAG ? (M16_STAG_RING == 6 ? 28 : 32) : 32)) * 1024;
   extern __shared__ __attribute__((aligned(16))) char lds[];  // [halo: 4 planes][W ring]
 
-  const int lin = blockIdx.x;
   int unit, widx;
   if (tl.xpu) {
     // XCD set su runs weight sets su*P .. su*P+P-1 (P = tl.pair, default 1); with P > 1 (Mconv1: its
@@ -599,6 +599,27 @@ __global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, Spli
   }
 }
 
+// PERS (round 6): a persistent grid of one workgroup per CU, each running the
+// tiles lin = blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so every tile keeps its XCD
+// and its place in the XCD-aware order): tile i's epilogue stores drain while tile i + 1 stages its
+// ring and first halo, instead of every CU writing its outputs in the same burst at the end of a
+// round of workgroups.  A barrier between tiles keeps the staggered half's last pair ahead of the
+// next tile's ring staging.
+template <int KS, int NPX, bool DEEP = false, bool STAG = false, bool CIRC = false, bool LIN = false, bool PERS = false>
+__global__ __launch_bounds__(512, 1) void conv_m16_bf16x3(SplitConvShape s, SplitConvGroup g0, SplitConvGroup g1,
+                                                          BigTiling tl) {
+  static_assert(!PERS || (LIN && !DEEP), "persistent tiles: the linear-halo kernel");
+  if constexpr (PERS) {
+#pragma unroll 1
+    for (int lin = blockIdx.x; lin < tl.pers_blocks; lin += gridDim.x) {
+      if (lin != (int)blockIdx.x) __syncthreads();
+      m16_tile<KS, NPX, DEEP, STAG, CIRC, LIN>(s, g0, g1, tl, lin);
+    }
+  } else {
+    m16_tile<KS, NPX, DEEP, STAG, CIRC, LIN>(s, g0, g1, tl, blockIdx.x);
+  }
+}
+
 int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const SplitConvGroup& g0,
                    const SplitConvGroup& g1, const BigTiling& tl) {
   static bool attr = false;
@@ -626,7 +647,12 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 9, false, true, false, true>,
                          (const void*)conv_m16_bf16x3<7, 8, false, true, false, true>,
                          (const void*)conv_m16_bf16x3<7, 7, false, true, false, true>,
-                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true>};
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, true, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 9, false, true, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, true, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 7, false, true, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -665,9 +691,29 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   const char* lin_env = getenv("OP_M16_LIN");
   const bool lin = stag && !deep && !circ && npx >= 6 && s.in_planar && s.pin == 3 && tl.pitch == s.w + 2 * s.pin &&
                    lin_env && atoi(lin_env) == 1;
+  // round 6: persistent tiles (PERS) for LIN launches of more than one round, unsplit (OP_M16_PERS=1,
+  // read per call)
+  const char* pers_env = getenv("OP_M16_PERS");
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    OP_HIP_CHECK(hipGetDevice(&dev));
+    OP_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const unsigned pgrid = (unsigned)(n_cu / 8 * 8);
+  const bool pers = lin && tl.ksplit == 1 && pgrid >= 8 && blocks > pgrid && pers_env && atoi(pers_env) == 1;
+  BigTiling tlp = tl;
+  tlp.pers_blocks = (int)blocks;
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_LAUNCH_C(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
-#define M16_LAUNCH_L(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
+#define M16_LAUNCH_L(N)                                                                                               \
+  do {                                                                                                                \
+    if (pers)                                                                                                         \
+      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true, true>), dim3(pgrid), dim3(512), lds, st, s, \
+                         g0, g1, tlp);                                                                                \
+    else                                                                                                              \
+      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true>), grid, dim3(512), lds, st, s, g0, g1, tl); \
+  } while (0)
 #define M16_CASE(N)                                  \
   case N:                                            \
     if (deep && N <= 5) {                            \
@@ -703,6 +749,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   census_add(stag ? OP_CENSUS_7X7_STAG : OP_CENSUS_7X7_PLAIN_RING);
   if (circ) census_add(OP_CENSUS_7X7_CIRC);
   if (lin) census_add(OP_CENSUS_7X7_LIN);
+  if (pers) census_add(OP_CENSUS_7X7_PERS);
 #if M16_STAMPS
   static const bool dump = getenv("OP_M16_STAMPS") != nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

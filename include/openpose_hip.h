@@ -330,6 +330,7 @@ int op_profile_classes(op_ctx* ctx, int32_t mask);
 #define OP_CENSUS_7X7_Q_IWG 35      /* conv_m16q launches with both tap ranges in one 8-wave workgroup (round 6) */
 #define OP_CENSUS_7X7_LIN 36        /* conv_m16 launches with linear halo sources (LIN, round 6) */
 #define OP_CENSUS_7X7_Q_BPF 37      /* conv_m16q launches with B fragments one tap ahead (round 6) */
+#define OP_CENSUS_7X7_PERS 38       /* conv_m16 launches as a persistent grid of one workgroup per CU (round 6) */
 #define OP_CENSUS_SLOTS 40
 int op_conv_census(int32_t* counts, int32_t n, int32_t reset);
 

@@ -383,24 +383,30 @@ def test_circular_halo_bit_identical(lib, bctx, monkeypatch, n):
 def test_linear_halo_sources_bit_identical(lib, bctx, monkeypatch, n):
     """Round 6: the staggered 7x7 kernel with linear halo sources (conv_m16.hip LIN: on chunk-planar
     input with the tight pitch a halo slot's source pixel is one linear index; OP_M16_LIN=0 keeps the
-    row / column cursor) loads the same pixels into the same LDS slots: the maps are bit-identical
-    at 38 frames and at the headline's 232, and the census shows LIN ran every 7x7 launch."""
+    row / column cursor), with the halo trimmed to a tile's own rows (OP_M16_TRIM) and as a
+    persistent grid (PERS, OP_M16_PERS) loads the same pixels into the slots the MFMAs read: the maps
+    are bit-identical at 38 frames and at the headline's 232, and the census shows LIN ran every 7x7
+    launch."""
     rng = np.random.default_rng(500 + n)
     x = rng.uniform(-0.5, 0.5, (n, 3, SIDE, SIDE)).astype(np.float32)
     out = {}
-    for lin, trim in (("1", "1"), ("1", "0"), ("0", "0")):  # trim: only a tile's own halo rows loaded
+    # trim: only a tile's own halo rows loaded; pers: a persistent grid of one workgroup per CU
+    for lin, trim, pers in (("1", "1", "1"), ("1", "1", "0"), ("1", "0", "0"), ("0", "0", "0")):
         monkeypatch.setenv("OP_M16_LIN", lin)
         monkeypatch.setenv("OP_M16_TRIM", trim)
+        monkeypatch.setenv("OP_M16_PERS", pers)
         _census_npx(lib)
-        out[lin + trim] = bctx.forward(x)
+        out[lin + trim + pers] = bctx.forward(x)
         cen = _census_npx(lib)
-        print("n %d OP_M16_LIN=%s OP_M16_TRIM=%s census:" % (n, lin, trim), cen)
+        print("n %d OP_M16_LIN=%s OP_M16_TRIM=%s OP_M16_PERS=%s census:" % (n, lin, trim, pers), cen)
         assert cen["7x7_stag"] == 25, cen
         assert cen["7x7_lin"] == (25 if lin == "1" else 0), cen
-    monkeypatch.delenv("OP_M16_LIN")
-    monkeypatch.delenv("OP_M16_TRIM")
-    for k in ("11", "10"):
-        for a, b in zip(out[k], out["00"]):
+        if pers == "1":  # launches of more than one round of workgroups (not 38 frames' Mconv1)
+            assert cen["7x7_pers"] > 0, cen
+    for k in ("OP_M16_LIN", "OP_M16_TRIM", "OP_M16_PERS"):
+        monkeypatch.delenv(k)
+    for k in ("111", "110", "100"):
+        for a, b in zip(out[k], out["000"]):
             assert np.array_equal(a, b), (k, float(np.abs(a - b).max()))
 
 
