@@ -84,7 +84,7 @@ __device__ __forceinline__ void m16_tile(const SplitConvShape& s, const SplitCon
                                          const BigTiling& tl, const int lin) {
   static_assert(!STAG || M16_DMA_HALF, "staggered halves: waves 4-7 must not stage the ring");
   static_assert(!CIRC || (STAG && !DEEP && KS == 7), "circular halo: the staggered 7x7 ring kernel only");
-  static_assert(!LIN || (STAG && !DEEP && !CIRC), "linear halo sources: the staggered drained kernel");
+  static_assert(!LIN || (!DEEP && !CIRC), "linear halo sources: the drained 4- / 6-tap ring kernels");
   constexpr int KSQ = KS * KS;
   constexpr int R = KS / 2;
   constexpr int CW = 128, PG = 4;        // 2 channel halves x 4 pixel groups = 8 waves
@@ -652,7 +652,17 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
                          (const void*)conv_m16_bf16x3<7, 9, false, true, false, true, true>,
                          (const void*)conv_m16_bf16x3<7, 8, false, true, false, true, true>,
                          (const void*)conv_m16_bf16x3<7, 7, false, true, false, true, true>,
-                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true, true>};
+                         (const void*)conv_m16_bf16x3<7, 6, false, true, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, false, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 9, false, false, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, false, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 7, false, false, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, false, false, true>,
+                         (const void*)conv_m16_bf16x3<7, 10, false, false, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 9, false, false, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 8, false, false, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 7, false, false, false, true, true>,
+                         (const void*)conv_m16_bf16x3<7, 6, false, false, false, true, true>};
     for (const void* f : fns)
       OP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -689,7 +699,7 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   // round 6: linear halo sources (LIN) on chunk-planar input with the tight pitch (OP_M16_LIN=1, read
   // per call)
   const char* lin_env = getenv("OP_M16_LIN");
-  const bool lin = stag && !deep && !circ && npx >= 6 && s.in_planar && s.pin == 3 && tl.pitch == s.w + 2 * s.pin &&
+  const bool lin = !deep && !circ && npx >= 6 && s.in_planar && s.pin == 3 && tl.pitch == s.w + 2 * s.pin &&
                    lin_env && atoi(lin_env) == 1;
   // round 6: persistent tiles (PERS) for LIN launches of more than one round, unsplit (OP_M16_PERS=1,
   // read per call)
@@ -706,13 +716,13 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   tlp.pers_blocks = (int)blocks;
 #define M16_LAUNCH(N, D, S) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, D, S>), grid, dim3(512), lds, st, s, g0, g1, tl)
 #define M16_LAUNCH_C(N) hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, true>), grid, dim3(512), lds, st, s, g0, g1, tl)
-#define M16_LAUNCH_L(N)                                                                                               \
+#define M16_LAUNCH_L(N, S)                                                                                            \
   do {                                                                                                                \
     if (pers)                                                                                                         \
-      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true, true>), dim3(pgrid), dim3(512), lds, st, s, \
+      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, S, false, true, true>), dim3(pgrid), dim3(512), lds, st, s,    \
                          g0, g1, tlp);                                                                                \
     else                                                                                                              \
-      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, true, false, true>), grid, dim3(512), lds, st, s, g0, g1, tl); \
+      hipLaunchKernelGGL((conv_m16_bf16x3<7, N, false, S, false, true>), grid, dim3(512), lds, st, s, g0, g1, tl);    \
   } while (0)
 #define M16_CASE(N)                                  \
   case N:                                            \
@@ -721,10 +731,11 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
       else M16_LAUNCH(N, (N <= 5), false);           \
     } else if (stag) {                               \
       if (circ && N >= 6) M16_LAUNCH_C((N >= 6 ? N : 6)); \
-      else if (lin && N >= 6) M16_LAUNCH_L((N >= 6 ? N : 6)); \
+      else if (lin && N >= 6) M16_LAUNCH_L((N >= 6 ? N : 6), true); \
       else M16_LAUNCH(N, false, true);               \
     } else {                                         \
-      M16_LAUNCH(N, false, false);                   \
+      if (lin && N >= 6) M16_LAUNCH_L((N >= 6 ? N : 6), false); \
+      else M16_LAUNCH(N, false, false);              \
     }                                                \
     break;
   switch (npx) {
@@ -738,8 +749,10 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
     M16_CASE(2)
     default:
       if (circ) M16_LAUNCH_C(10);
-      else if (lin) M16_LAUNCH_L(10);
-      else if (stag) M16_LAUNCH(10, false, true);
+      else if (lin) {
+        if (stag) M16_LAUNCH_L(10, true);
+        else M16_LAUNCH_L(10, false);
+      } else if (stag) M16_LAUNCH(10, false, true);
       else M16_LAUNCH(10, false, false);
   }
 #undef M16_CASE
