@@ -441,7 +441,23 @@ def test_staggered_halves_precise_720p(lib, monkeypatch):
             out[stag] = c.fetch_maps(0, 2)
         monkeypatch.delenv("OP_M16_STAG")
         monkeypatch.delenv("OP_M16_CIRC")
-        for other in ("0", "circ0"):
+        # round 6: linear halo sources, trimmed halos and the persistent grid on these wide maps too
+        # (frame-aligned tiles on the unstaggered ring included)
+        for k, v in (("OP_M16_LIN", "1"), ("OP_M16_TRIM", "1"), ("OP_M16_PERS", "1")):
+            monkeypatch.setenv(k, v)
+        c.stage_frames(frames)
+        _census_npx(lib)
+        try:
+            c.run_staged_precise()
+        except IndexError:
+            pass
+        c.synchronize()
+        cen = _census_npx(lib)
+        assert cen["7x7_lin"] > 0 and cen["7x7_pers"] > 0, cen
+        out["lin"] = c.fetch_maps(0, 2)
+        for k in ("OP_M16_LIN", "OP_M16_TRIM", "OP_M16_PERS"):
+            monkeypatch.delenv(k)
+        for other in ("0", "circ0", "lin"):
             for a, b in zip(out["1"], out[other]):
                 assert np.array_equal(a, b), (other, float(np.abs(a - b).max()))
     finally:
