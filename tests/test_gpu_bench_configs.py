@@ -453,7 +453,7 @@ def test_staggered_halves_precise_720p(lib, monkeypatch):
             pass
         c.synchronize()
         cen = _census_npx(lib)
-        assert cen["7x7_lin"] > 0 and cen["7x7_pers"] > 0, cen
+        assert cen["7x7_lin"] > 0, cen  # (2 frames: every launch within one round, so no PERS grid)
         out["lin"] = c.fetch_maps(0, 2)
         for k in ("OP_M16_LIN", "OP_M16_TRIM", "OP_M16_PERS"):
             monkeypatch.delenv(k)
