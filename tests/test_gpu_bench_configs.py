@@ -401,8 +401,8 @@ def test_linear_halo_sources_bit_identical(lib, bctx, monkeypatch, n):
         print("n %d OP_M16_LIN=%s OP_M16_TRIM=%s OP_M16_PERS=%s census:" % (n, lin, trim, pers), cen)
         assert cen["7x7_stag"] == 25, cen
         assert cen["7x7_lin"] == (25 if lin == "1" else 0), cen
-        if pers == "1":  # launches of more than one round of workgroups (not 38 frames' Mconv1)
-            assert cen["7x7_pers"] > 0, cen
+        if pers == "1" and n == 232:  # launches of more than one round (38 frames: 252 workgroups)
+            assert cen["7x7_pers"] == 25, cen
     for k in ("OP_M16_LIN", "OP_M16_TRIM", "OP_M16_PERS"):
         monkeypatch.delenv(k)
     for k in ("111", "110", "100"):
