@@ -908,9 +908,11 @@ static int launch_conv_m16q(const SplitConvShape& s, const SplitConvGroup* g, in
   if (s.in_planar) census_add(OP_CENSUS_7X7_PLANAR);
   const SplitConvGroup& g1 = s.groups > 1 ? g[1] : g[0];
   if (iwg) census_add(OP_CENSUS_7X7_Q_IWG);
-  // round 6: B fragments one tap ahead (OP_M16Q_BPF=1, read per launch)
+  // round 6: B fragments one tap ahead, by default (OP_M16Q_BPF=0, read per launch, reads them at the
+  // tap): one frame's 7x7 class 0.950-0.968 -> 0.943-0.959 ms in 5 interleaved rounds on two boxes
+  // (profiles/r06/ab_r06r_b1_m16q_bpf_split_wg.log, ab_r06t_b1_m16q_bpf.log); bit-identical
   const char* bpf_env = getenv("OP_M16Q_BPF");
-  const bool bpf = !iwg && tr == 4 && nth == 2 && pfk == 2 && bpf_env && atoi(bpf_env) == 1;
+  const bool bpf = !iwg && tr == 4 && nth == 2 && pfk == 2 && !(bpf_env && atoi(bpf_env) == 0);
   if (bpf) census_add(OP_CENSUS_7X7_Q_BPF);
   const int rc = launch_m16q_7x7(tr, nth, pfk, st, s, g[0], g1, t, iwg, bpf);
   if (rc != OP_OK) return rc;
@@ -1070,9 +1072,10 @@ int launch_conv_big(const SplitConvShape& s, const SplitConvGroup* g, hipStream_
         tl.pair = 1;
       }
       tl.zeros = device_zeros();
-      // round 6: LIN tiles within one frame load only their own halo rows (OP_M16_TRIM, read per launch)
+      // round 6: LIN tiles within one frame load only their own halo rows (default; OP_M16_TRIM=0, read
+      // per launch, loads the plane's nh pieces sized for the frame-crossing tiles)
       const char* trim_env = getenv("OP_M16_TRIM");
-      tl.halo_trim = trim_env && atoi(trim_env) == 1;
+      tl.halo_trim = !(trim_env && atoi(trim_env) == 0);
       if (!tl.zeros) {
         set_error("conv_m16_bf16x3: conv_big_device_init was not called for this device");
         return OP_ERR_STATE;

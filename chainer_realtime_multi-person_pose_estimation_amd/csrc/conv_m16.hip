@@ -696,13 +696,16 @@ int launch_m16_7x7(int npx, hipStream_t st, const SplitConvShape& s, const Split
   // (incremental staging cursor: 76.0 -> 80.4 ms, profiles/r06/ab_r06c_incr_scalar_cursor_not_kept.log)
   const char* circ_env = getenv("OP_M16_CIRC");
   const bool circ = stag && !deep && npx >= 6 && circ_env && atoi(circ_env) == 1;
-  // round 6: linear halo sources (LIN) on chunk-planar input with the tight pitch (OP_M16_LIN=1, read
-  // per call)
+  // round 6: linear halo sources (LIN) on chunk-planar input with the tight pitch, by default
+  // (OP_M16_LIN=0, read per call, keeps the row / column cursor): with the halo trimmed to a tile's own
+  // rows (conv_big.hip halo_trim) the headline's 7x7 class 74.9 -> 74.4 ms per step, C5's 39.6 ->
+  // 38.0, C4's within noise (profiles/r06/ab_r06t_7x7_lin_trim_pers_*.log); bit-identical
   const char* lin_env = getenv("OP_M16_LIN");
   const bool lin = !deep && !circ && npx >= 6 && s.in_planar && s.pin == 3 && tl.pitch == s.w + 2 * s.pin &&
-                   lin_env && atoi(lin_env) == 1;
-  // round 6: persistent tiles (PERS) for LIN launches of more than one round, unsplit (OP_M16_PERS=1,
-  // read per call)
+                   !(lin_env && atoi(lin_env) == 0);
+  // round 6: persistent tiles (PERS) for LIN launches of more than one round, unsplit (opt-in
+  // OP_M16_PERS=1, read per call): bit-identical, measured SLOWER -- the headline's 7x7 class 74.4 ->
+  // 77.4 ms per step, C5 38.0 -> 38.8 (profiles/r06/ab_r06t_7x7_lin_trim_pers_*.log)
   const char* pers_env = getenv("OP_M16_PERS");
   static int n_cu = 0;
   if (!n_cu) {
