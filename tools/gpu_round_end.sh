@@ -5,11 +5,14 @@
 # this tree's sets (bench.py committed_traffic); then smoke, the whole GPU suite, the bench lines, the
 # SQ and clock / MFMA-busy passes and the fabric reads by request size -- each PMC pass a run of its
 # own, each step under its own time limit, the first failure ending the call.
-#   usage: tools/gpu_round_end.sh TAG   (e.g. r06z; copies land in gpurun_out/final_TAG/)
+#   usage: tools/gpu_round_end.sh TAG [PART]   (e.g. r06z; copies land in gpurun_out/final_TAG/)
+#   PART: all (default); prof = the PMC sets, smoke and the bench lines; rest = the suite and the SQ /
+#   clock / TCC passes (two calls that each fit gpurun's time limit)
 set -o pipefail
-TAG=$1; R=${TAG:0:3}
+TAG=$1; PART=${2:-all}; R=${TAG:0:3}
 O=$GRAFT_REPO_ROOT/gpurun_out/final_$TAG; mkdir -p $O
 cd $GRAFT_REPO_ROOT
+if [ "$PART" != rest ]; then
 for spec in "${TAG}_m4_b232|" "${TAG}_c5_m4_b64|--frame 720x1280" "${TAG}_c4_m4_b16|--precise --frame 720x1280"; do
   nm=${spec%%|*}; args=${spec#*|}
   echo "[$(date +%T)] profile $nm $args"
@@ -19,14 +22,17 @@ for spec in "${TAG}_m4_b232|" "${TAG}_c5_m4_b64|--frame 720x1280" "${TAG}_c4_m4_
 done
 echo "[$(date +%T)] smoke"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
-echo "[$(date +%T)] suite"
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $O/suite.log 2>&1 || exit $?
-tail -2 $O/suite.log
 echo "[$(date +%T)] lines"
 bash tools/gpu_lines.sh $TAG || exit $?
 cp gpurun_out/lines_$TAG/*.log gpurun_out/lines_$TAG/lines.jsonl $O/ || exit $?
+fi
+if [ "$PART" != prof ]; then
+echo "[$(date +%T)] suite"
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $O/suite.log 2>&1 || exit $?
+tail -2 $O/suite.log
 echo "[$(date +%T)] sq / clk / tcc"
 bash tools/sq_counters.sh $TAG || exit $?
 bash tools/clk_counters.sh $TAG --no-variants || exit $?
 bash tools/gpu_tcc_bytes.sh $TAG || exit $?
+fi
 echo done
