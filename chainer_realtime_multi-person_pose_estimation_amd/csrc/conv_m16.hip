@@ -217,12 +217,13 @@ __device__ __forceinline__ void m16_tile(const SplitConvShape& s, const SplitCon
       const int lastA = (hp_in - T.y0) * wp_in - 1;
       const char* const a0 = src0 + (int64_t)T.y0 * wp_in * 16;
       char* dst = halo + h_plane * HPLANE + h_i0 * 1024;
-      // halo_trim: a tile within one frame reads halo slots < its rows x pitch only (its output rows +
-      // 2R; block q = (y - y0) * pitch + x plus tap offsets < 2R * pitch + 2R): the pieces past them
-      // (the plane is sized for the frame-crossing tiles' extra 2R rows) are not loaded
+      // halo_trim: a tile reads halo slots < its rows x pitch only (its output rows + 2R, or for a tile
+      // that crosses a frame both row sets; block q = (y - y0) * pitch + x plus tap offsets < 2R * pitch
+      // + 2R): the pieces past them (the plane is sized for the launch's largest tile) are not loaded
       int np = tl.nh;
-      if (tl.halo_trim && T.fb == T.frame) {
-        const int rows = (T.P1 - T.frame * tl.hw) / s.w - T.y0 + 1 + 2 * R;
+      if (tl.halo_trim) {  // a tile that crosses a frame: frame A's rowsA rows, then frame B's rows 0..yb + 2R
+        const int yb = (T.P1 - T.fb * tl.hw) / s.w;
+        const int rows = T.fb == T.frame ? yb - T.y0 + 1 + 2 * R : T.rowsA + yb + 1 + 2 * R;
         np = min(np, (rows * tl.pitch + 63) / 64);
       }
       for (int i = h_i0; i < np; i += 2) {
